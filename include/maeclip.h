@@ -1,0 +1,303 @@
+/* libmaeclip -- C-ABI of the MI355X (gfx950) kernels behind the mae_clip hot path.
+ *
+ * The reference (ykojima4020/mae_clip) has no FFI: its boundary is the PyTorch
+ * nn.Module API of modules.ImageEncoder / TextEncoder / ProjectionHead
+ * (modules.py:8-76) and CLIP.CLIPModel (CLIP.py:9-52), which calls into
+ * timm / HF transformers / torch ops. Each entry point below replaces the op
+ * those modules dispatch (cited per function); the Python package
+ * mae_clip_amd binds them with ctypes.
+ *
+ * Conventions
+ *   - plain pointers + sizes; every pointer is device memory unless noted;
+ *     bf16 tensors are uint16 bit patterns; strides are in elements.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream).
+ *   - no entry point allocates, frees or synchronises (graph-capture safe);
+ *     workspaces are provided by the caller.
+ *   - return 0 on success, <0 on error; maeclip_last_error() gives the
+ *     message (thread-local).
+ */
+#ifndef MAECLIP_H
+#define MAECLIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAECLIP_ABI_VERSION 1
+#ifndef MAECLIP_F32
+#define MAECLIP_F32 0
+#define MAECLIP_BF16 1
+#endif
+
+int32_t maeclip_abi_version(void);
+const char* maeclip_last_error(void);
+/* number of gfx950 devices visible (0 when no GPU); does not create a context */
+int32_t maeclip_device_count(void);
+
+/* ------------------------------------------------------------------ GEMM
+ * Replaces torch.nn.functional.linear (cuBLAS) for every nn.Linear on the
+ * hot path (timm Block qkv/proj/fc1/fc2, PatchEmbed conv-as-GEMM,
+ * modules.py:64-66 ProjectionHead, DistilBERT q/k/v/out/lin1/lin2, HF ViTMAE
+ * decoder_embed/decoder_pred) in forward, dgrad and wgrad form, and the
+ * N x N x P products of the CLIP loss (CLIP.py:34-38).
+ *   C[z][m][n] = alpha * sum_k A(m,k) B(k,n) (+bias[n]) (epilogue) (+beta*C)
+ * layouts: 0 = K-contiguous (A[m*lda+k], B[n*ldb+k]); 1 = row-contiguous
+ * (A[k*lda+m], B[k*ldb+n]).
+ * epilogue: 0 none; 1 GELU (aux_out <- pre-activation, C <- gelu(pre));
+ *           2 residual (C(f32) <- resid + acc (+bias)); 3 dGELU (C <- acc *
+ *           gelu'(aux) (+ resid if resid != NULL)).
+ * colsum_partial (optional, f32 [batch*maeclip_gemm_colsum_rows(M)][N]):
+ *   per-block column sums of the final C, reduce with maeclip_colsum_reduce. */
+typedef struct {
+  const void* A;
+  const void* B;
+  void* C;
+  int64_t M, N, K;
+  int64_t lda, ldb, ldc;
+  int64_t batch, strideA, strideB, strideC;
+  int32_t dtype;     /* MAECLIP_F32 = 0 / MAECLIP_BF16 = 1 (A, B, aux) */
+  int32_t out_dtype; /* C */
+  int32_t a_layout, b_layout;
+  int32_t epilogue;
+  float alpha, beta;
+  const float* bias;
+  const void* aux;
+  void* aux_out;
+  int64_t ldaux;
+  const float* resid;
+  int64_t ldr;
+  float* colsum_partial;
+} maeclip_gemm_args;
+int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
+int64_t maeclip_gemm_colsum_rows(int64_t M);
+
+/* ------------------------------------------------------------- attention
+ * Replaces F.scaled_dot_product_attention in timm Attention / HF ViTMAE
+ * decoder layers and DistilBERT attention with key-padding mask
+ * (modeling_distilbert.py:125-145). qkv: [B*n, ld_qkv] token rows with q at
+ * column h*hd, k at H*hd + h*hd, v at 2*H*hd + h*hd. o: [B*n, ld_o].
+ * lse: [B, H, n] f32, log2-domain row log-sum-exp of scale*q.k (bwd input).
+ * key_mask (optional, f32 [B, n]): 0 = padding key. dropout_p applies to the
+ * probabilities in the forward only (DistilBERT attention dropout; no bwd).
+ * bwd: dout [B*n, ld_o], dqkv [B*n, ld_dqkv]; colsum_partial optional
+ * [B, 3*H*hd] per-sample column sums of dqkv (qkv bias gradient). */
+typedef struct {
+  const void* qkv;
+  void* o;
+  float* lse;
+  const void* dout;
+  void* dqkv;
+  const float* key_mask;
+  float* colsum_partial;
+  int64_t ld_qkv, ld_o, ld_dqkv;
+  int32_t B, n, H, head_dim, dtype;
+  float scale, dropout_p;
+  uint64_t seed;
+} maeclip_attn_args;
+int32_t maeclip_attn_fwd(const maeclip_attn_args* args, void* stream);
+int32_t maeclip_attn_bwd(const maeclip_attn_args* args, void* stream);
+
+/* ------------------------------------------------------------- LayerNorm
+ * Replaces nn.LayerNorm (timm norm1/norm2/fc_norm, modules.py:67, DistilBERT
+ * LayerNorms, decoder_norm). fwd: x' = dropout(x; in_dropout_p) + res;
+ * y = LN(x') (* out dropout); y2 optional bf16 copy; xsum_out optional x'. */
+typedef struct {
+  const void* x;
+  int32_t x_dtype;
+  const float* res;
+  int64_t ldres;
+  float in_dropout_p;
+  const float* gamma;
+  const float* beta;
+  void* y;
+  int32_t y_dtype;
+  void* y2;
+  int64_t ldy2;
+  float* xsum_out;
+  int64_t ldxs;
+  float* mean;
+  float* rstd;
+  float out_dropout_p;
+  uint64_t seed_in, seed_out;
+  int64_t M, D, ldx, ldy;
+  float eps;
+} maeclip_ln_fwd_args;
+int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* args, void* stream);
+
+/* bwd: dx(f32) = LN'(dy) + dres; dx_bf optional bf16 copy; partials
+ * [maeclip_ln_bwd_partial_rows(M)][D] of dgamma, dbeta, colsum(dx). */
+typedef struct {
+  const void* dy;
+  int32_t dy_dtype;
+  const void* x;
+  int32_t x_dtype;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* dres;
+  float* dx;
+  void* dx_bf;
+  int64_t lddx_bf;
+  float* dgamma_partial;
+  float* dbeta_partial;
+  float* dx_colsum_partial;
+  int64_t M, D, ldx, lddy, lddx;
+} maeclip_ln_bwd_args;
+int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* args, void* stream);
+int32_t maeclip_ln_bwd_partial_rows(int64_t M);
+
+/* ------------------------------------------------------------ reductions */
+/* out[n] (+)= scale * sum_p partial[p*N + n]  (fixed order -> deterministic) */
+int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate, float scale,
+                              void* stream);
+/* partial column sums of a [M, D] row matrix (dtype f32/bf16, row stride ld)
+ * into partial [maeclip_rows_colsum_partial_rows(M)][D]; optional bf16 copy
+ * out_bf16 [M, D]. */
+int32_t maeclip_rows_colsum(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld, void* out_bf16,
+                            float* partial, void* stream);
+int32_t maeclip_rows_colsum_partial_rows(int64_t M);
+/* timm global_pool="avg": out[b] = mean_{t>=1} x[b,t,:] ; bwd scatters 1/(n-1) */
+int32_t maeclip_pool_fwd(const float* x, int32_t B, int32_t n, int32_t D, float* out, void* stream);
+int32_t maeclip_pool_bwd(const float* dout, int32_t B, int32_t n, int32_t D, float* dx, int32_t accumulate, void* stream);
+/* nn.Dropout with the library's counter-based mask (same as LN in_dropout) */
+int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed, void* stream);
+/* DistilBERT Embeddings word+position gather (modeling_distilbert.py:92-117) */
+int32_t maeclip_embed_fwd(const int64_t* ids, const float* word, const float* pos, int32_t B, int32_t T, int32_t D,
+                          int64_t V, float* out, void* stream);
+
+/* ---------------------------------------------------------- multi-tensor */
+typedef struct {
+  void* p0; /* param (f32) / cast source */
+  void* p1; /* grad (f32) */
+  void* p2; /* exp_avg */
+  void* p3; /* exp_avg_sq */
+  void* p4; /* bf16 shadow / cast destination (optional for adamw) */
+  int64_t n;
+  int64_t chunk_start; /* prefix sum of ceil(n / maeclip_mt_chunk()) */
+} maeclip_mt_entry;
+typedef struct {
+  float lr, beta1, beta2, eps, weight_decay;
+  float step_size; /* lr / (1 - beta1^t) */
+  float bc2_sqrt;  /* sqrt(1 - beta2^t) */
+  float grad_scale;
+} maeclip_adamw_hparams;
+int64_t maeclip_mt_chunk(void);
+/* dev_entries: device copy of host_entries (host pointer used for the grid size) */
+int32_t maeclip_cast_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries, int32_t ne,
+                           void* stream);
+/* torch.optim.AdamW step (main.py:101-103,59) fused over all parameters */
+int32_t maeclip_adamw_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries, int32_t ne,
+                            const maeclip_adamw_hparams* hp, void* stream);
+
+/* ------------------------------------------------------------------- MAE */
+/* HF ViTMAE random_masking (modeling_vit_mae.py:297-327) with counter-based
+ * noise: ids int32 [B, L]; mask f32 [B, L] (1 = removed); noise optional. */
+typedef struct {
+  int32_t* ids_shuffle;
+  int32_t* ids_restore;
+  float* mask;
+  float* noise;
+  int32_t B, L, len_keep;
+  uint64_t seed, step, sample_offset;
+} maeclip_mask_args;
+int32_t maeclip_mask_ids(const maeclip_mask_args* args, void* stream);
+
+/* visible-patch rows for the patch-embed GEMM (timm PatchEmbed Conv2d(k=s=p)
+ * as GEMM): out[(b*keep+j), c*p*p+ky*p+kx] = img[b,c,py*p+ky,px*p+kx] for
+ * patch l = ids_shuffle[b,j] (identity if NULL); columns >= C*p*p zeroed. */
+typedef struct {
+  const float* img;
+  const int32_t* ids_shuffle;
+  void* out;
+  int64_t ld_out;
+  int32_t B, C, S, p, keep, dtype;
+} maeclip_patch_args;
+int32_t maeclip_patch_gather(const maeclip_patch_args* args, void* stream);
+
+/* timm _pos_embed on the visible tokens: x[b,0] = cls + pos[0];
+ * x[b,1+j] = y[b*keep+j] + pos[1+ids_shuffle[b,j]]; bwd: dy rows, dpos, dcls. */
+typedef struct {
+  const void* y;
+  int64_t ldy;
+  const int32_t* ids_shuffle;
+  const int32_t* ids_restore;
+  const float* pos;
+  const float* cls;
+  float* x;
+  const float* dx;
+  void* dy;
+  float* dpos;
+  float* dcls;
+  int32_t B, L, keep, D, dtype;
+} maeclip_tokens_args;
+int32_t maeclip_tokens_fwd(const maeclip_tokens_args* args, void* stream);
+int32_t maeclip_tokens_bwd(const maeclip_tokens_args* args, void* stream);
+
+/* HF ViTMAEDecoder mask-token append + unshuffle + pos (modeling_vit_mae.py:548-566).
+ * fwd: y f32 [B, 1+keep, ldy] -> out f32 [B, 1+L, D]. bwd: dout f32 -> dy
+ * (dtype) [B, 1+keep, ldy], dmask_partial / colsum_partial f32 [B, D]. */
+typedef struct {
+  const float* y;
+  int64_t ldy;
+  const int32_t* ids_shuffle;
+  const int32_t* ids_restore;
+  const float* mask_token;
+  const float* pos;
+  float* out;
+  const float* dout;
+  void* dy;
+  float* dmask_partial;
+  float* colsum_partial;
+  int32_t B, L, keep, D, dtype;
+} maeclip_unshuffle_args;
+int32_t maeclip_unshuffle_fwd(const maeclip_unshuffle_args* args, void* stream);
+int32_t maeclip_unshuffle_bwd(const maeclip_unshuffle_args* args, void* stream);
+
+/* MAE reconstruction loss (modeling_vit_mae.py:706-745 patchify, :852-859).
+ * pred: decoder output rows [B, 1+L, ldp] (row 0 = cls, ignored); targets are
+ * patchified from img on the fly. fwd: row_loss [B*L] = mask * mean_k diff^2
+ * (sum / mask_count outside). bwd: dpred [B, 1+L, lddp] = grad_out[0] *
+ * loss_scale * 2 diff mask / (P * mask_count); colsum_partial [B, P] optional. */
+typedef struct {
+  const void* pred;
+  int64_t ldp;
+  const float* img;
+  const float* mask;
+  float* row_loss;
+  void* dpred;
+  int64_t lddp;
+  const float* grad_out;
+  float* colsum_partial;
+  float loss_scale, mask_count;
+  int32_t B, C, S, p, L, norm_pix, dtype;
+} maeclip_mae_loss_args;
+int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* args, void* stream);
+int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* args, void* stream);
+
+/* ------------------------------------------------------------- CLIP loss
+ * CLIPModel.forward loss (CLIP.py:34-43) + cross_entropy (CLIP.py:46-52), fp32.
+ * I, T: [N, P] (row strides ld_I/ld_T, 0 = P). loss: device scalar.
+ * dI, dT optional (d loss / d I, T; computed in the same call). */
+typedef struct {
+  const float* I;
+  const float* T;
+  int64_t ld_I, ld_T;
+  int64_t N, P;
+  float temperature;
+  float* loss;
+  float* row_loss_out;
+  float* dI;
+  float* dT;
+  int64_t ld_dI, ld_dT;
+  void* workspace;
+  size_t ws_bytes;
+} maeclip_clip_args;
+size_t maeclip_clip_loss_workspace(int64_t N);
+int32_t maeclip_clip_loss(const maeclip_clip_args* args, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAECLIP_H */

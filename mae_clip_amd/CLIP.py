@@ -1,0 +1,152 @@
+"""Drop-in for the reference's CLIP.py (CLIP.py:9-52): CLIPModel + cross_entropy.
+
+CLIPModel.forward(batch) -> 0-d loss, exactly the reference contract used by
+main.py:56-59 (model(batch); loss.backward(); optimizer.step()) and
+main.py:76 (no_grad eval). With config.mask_ratio > 0 the MAE head of
+BASELINE.json is added: the encoder runs once on the
+visible patches (FLIP-style), the CLIP image feature is the mean over visible
+patch tokens -> fc_norm, the decoder reconstructs the masked patches and
+loss = clip + mae_weight * mae. With mask_ratio == 0 the path is the
+reference's CLIP path exactly.
+
+Data parallel (one process per GPU): if torch.distributed is initialised and
+`model.process_group` is set (mae_clip_amd.distributed.DataParallel does it),
+the projection embeddings are all-gathered so the contrastive loss uses the
+global batch, and the MAE term's gradient is scaled by 1/world so that a SUM
+all-reduce of parameter gradients yields the exact global-batch gradient.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from . import config as CFG
+from . import functions as Fn
+from . import kernels as K
+from .modules import (ImageEncoder, TextEncoder, ProjectionHead, MAEDecoder, WeightCache, compute_dtype,
+                      run_stack)
+
+
+class CLIPModel(nn.Module):
+    def __init__(self, temperature=None, image_embedding=None, text_embedding=None):
+        super().__init__()
+        temperature = CFG.temperature if temperature is None else temperature
+        image_embedding = image_embedding or CFG.image_embedding
+        text_embedding = text_embedding or CFG.text_embedding
+        self.image_encoder = ImageEncoder()
+        self.text_encoder = TextEncoder()
+        if self.image_encoder.model.embed_dim != image_embedding:
+            raise ValueError(f"image_embedding={image_embedding} but {CFG.model_name} has "
+                             f"{self.image_encoder.model.embed_dim} features")
+        self.image_projection = ProjectionHead(embedding_dim=image_embedding)
+        self.text_projection = ProjectionHead(embedding_dim=text_embedding)
+        self.temperature = temperature
+        self.mask_ratio = CFG.mask_ratio
+        self.mae_weight = CFG.mae_weight
+        self.norm_pix_loss = CFG.norm_pix_loss
+        self.precision = CFG.precision
+        self.mask_seed = CFG.mask_seed
+        self.dropout_seed = CFG.dropout_seed
+        vit = self.image_encoder.model
+        if self.mask_ratio > 0:
+            self.mae_decoder = MAEDecoder(vit.embed_dim, vit.patch_embed.num_patches, vit.patch_embed.patch_size)
+        else:
+            self.mae_decoder = None
+        self.step = 0
+        self.last_losses = {}
+        self.process_group = None
+        self._cache = None
+
+    # ------------------------------------------------------------------
+    def _weight_cache(self):
+        if self._cache is None:
+            c = WeightCache()
+            self.image_encoder.model.register_weights(c)
+            if self.mae_decoder is not None:
+                self.mae_decoder.register_weights(c)
+            self._cache = c
+        return self._cache
+
+    def _world(self):
+        pg = self.process_group
+        if pg is None or not torch.distributed.is_initialized():
+            return 1, 0
+        return torch.distributed.get_world_size(pg), torch.distributed.get_rank(pg)
+
+    def masking(self, B, step, sample_offset, device):
+        vit = self.image_encoder.model
+        L = vit.patch_embed.num_patches
+        keep = int(L * (1 - self.mask_ratio))
+        ids_shuffle, ids_restore, mask, _ = K.mask_ids(B, L, keep, self.mask_seed, step, sample_offset, device)
+        return ids_shuffle, ids_restore, mask, keep
+
+    def forward(self, batch):
+        img = batch["image"]
+        if not img.is_cuda:
+            raise RuntimeError("mae_clip_amd.CLIPModel needs the batch on a ROCm device (no CPU fallback)")
+        dtype = compute_dtype(self.precision)
+        cache = self._weight_cache()
+        cache.refresh(dtype)
+        vit = self.image_encoder.model
+        B = img.shape[0]
+        world, rank = self._world()
+        step = self.step
+        seed = (self.dropout_seed * 1000003 + step * 8191 + rank) & 0x7FFFFFFFFFFFFFFF
+        mae = self.mae_decoder is not None
+        if mae:
+            ids_shuffle, ids_restore, mask, keep = self.masking(B, step, rank * B, img.device)
+            tokens = vit.forward_tokens(img, dtype, cache, ids_shuffle, ids_restore, keep)
+            dec = self.mae_decoder
+            feat, latent = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias,
+                                                  dec.mae_norm.weight, dec.mae_norm.bias)
+        else:
+            tokens = vit.forward_tokens(img, dtype, cache)
+            feat = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias, None, None)
+        text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17, dtype=dtype)
+        image_embeddings = self.image_projection(feat, seed=seed + 29)
+        text_embeddings = self.text_projection(text_features, seed=seed + 31)
+        if world > 1:
+            from .distributed import gather_rows
+            image_embeddings = gather_rows(image_embeddings, self.process_group)
+            text_embeddings = gather_rows(text_embeddings, self.process_group)
+        clip = clip_loss(image_embeddings, text_embeddings, self.temperature)
+        loss = clip
+        self.last_losses = {"clip": clip.detach()}
+        if mae:
+            L = vit.patch_embed.num_patches
+            dspec = Fn.DecSpec(B=B, L=L, keep=keep, dtype=dtype, w_T=cache.get(dec.decoder_embed.weight, dtype))
+            xd = Fn.DecoderEmbedFn.apply(latent, ids_shuffle, ids_restore, dspec, dec.decoder_embed.weight,
+                                         dec.decoder_embed.bias, dec.mask_token, dec.decoder_pos_embed)
+            xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache)
+            hspec = Fn.MaeHeadSpec(p=vit.patch_embed.patch_size, norm_pix=self.norm_pix_loss,
+                                   mask_count=float(B * (L - keep)), loss_scale=1.0 / world, dtype=dtype,
+                                   w_T=cache.get(dec.decoder_pred.weight, dtype))
+            ml = Fn.MaeHeadLossFn.apply(xd, img if img.dtype == torch.float32 else img.float(), mask, hspec,
+                                        dec.decoder_norm.weight, dec.decoder_norm.bias, dec.decoder_pred.weight,
+                                        dec.decoder_pred.bias)
+            self.last_losses["mae"] = ml.detach()
+            loss = clip + self.mae_weight * ml
+            self.last_mask = (ids_shuffle, ids_restore, mask)
+        if self.training:
+            self.step += 1
+        return loss
+
+
+def clip_loss(image_embeddings, text_embeddings, temperature=1.0):
+    """CLIP.py:34-43 on the fused fp32 kernel."""
+    if torch.is_grad_enabled() and (image_embeddings.requires_grad or text_embeddings.requires_grad):
+        return Fn.ClipLossFn.apply(image_embeddings, text_embeddings, temperature)
+    loss, _, _ = K.clip_loss(image_embeddings.contiguous(), text_embeddings.contiguous(), temperature,
+                             want_grad=False)
+    return loss
+
+
+def cross_entropy(preds, targets, reduction="none"):
+    """CLIP.py:46-52, kept for API compatibility (not used on the fused path)."""
+    log_softmax = nn.LogSoftmax(dim=-1)
+    loss = (-targets * log_softmax(preds)).sum(1)
+    if reduction == "none":
+        return loss
+    elif reduction == "mean":
+        return loss.mean()

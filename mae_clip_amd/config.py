@@ -1,0 +1,68 @@
+"""Flag system, same names as the reference's config.py (config.py:1-36).
+
+Changes vs the reference, all recorded in DESIGN.md:
+  * model_name / image_embedding default to the ViT-B/16 of BASELINE.json
+    (the reference default is timm resnet50 / 2048, config.py:15-16);
+  * pretrained = False: hub weights are fetch-by-name and unavailable offline;
+  * added: MAE head flags (mask_ratio, mae_weight, norm_pix_loss, decoder_*),
+    text_layers, precision, seeds.
+"""
+import torch
+
+debug = True
+image_path = "/data/yuto/clip/OpenAI-CLIP/dataset/coco"
+captions_path = "C:/Moein/AI/Datasets/Flicker-8k"
+batch_size = 8
+num_workers = 0
+lr = 1e-3
+weight_decay = 1e-3
+patience = 2
+factor = 0.5
+epochs = 10
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+model_name = "vit_base_patch16_224"
+image_embedding = 768
+text_encoder_model = "distilbert-base-uncased"
+text_embedding = 768
+text_tokenizer = "distilbert-base-uncased"
+max_length = 200
+
+pretrained = False  # reference: True (hub download); no network here
+trainable = True
+temperature = 1.0
+
+# image size
+size = 224
+
+# for projection head; used for both image and text encoders
+num_projection_layers = 1
+projection_dim = 256
+dropout = 0.1
+
+# log
+logdir = "./output/vit_mae_clip_amd"
+checkpoints = "./output/vit_mae_clip_amd/checkpoints/"
+
+# ---- added for the MAE head (BASELINE.json; HF ViTMAEConfig defaults)
+mask_ratio = 0.75          # 0 => CLIP-only, no shuffle, no decoder (== reference path)
+mae_weight = 1.0           # loss = clip + mae_weight * mae
+norm_pix_loss = False
+decoder_embed_dim = 512
+decoder_depth = 8
+decoder_num_heads = 16
+decoder_mlp_ratio = 4.0
+
+# ---- text encoder (DistilBertConfig defaults; C0 uses 2 layers)
+text_layers = 6
+text_heads = 12
+text_hidden = 3072
+text_vocab_size = 30522
+text_max_position = 512
+text_dropout = 0.1
+text_attention_dropout = 0.1
+
+# ---- numerics / determinism
+precision = "bf16"         # "bf16" (perf) or "fp32" (parity mode, exact-f32 MFMA)
+mask_seed = 2
+dropout_seed = 1234

@@ -1,0 +1,501 @@
+// Multi-head attention forward/backward (gfx950 MFMA).
+//
+// Replaces F.scaled_dot_product_attention inside timm's Attention (ViT encoder
+// blocks, timm 0.9.12), HF ViTMAE decoder layers (modeling_vit_mae.py:455-580)
+// and DistilBERT's self-attention with additive key-padding mask
+// (modeling_distilbert.py:125-145, 174-205).
+//
+// Input is the fused qkv activation [B*n, ld_qkv] (token rows; q at column
+// h*HD, k at H*HD + h*HD, v at 2*H*HD + h*HD) exactly as the qkv GEMM wrote
+// it, so no permute/copy kernels sit between the GEMM and attention.
+//
+// One workgroup (8 waves) owns one (sample, head): the whole K/V (and for the
+// backward Q/dO) slice of that head lives in LDS (n <= ~600 tokens fits for
+// every config: ViT-B 197/50, decoder 197/577 at HD=32, text 25).
+//   forward : waves take 16-query tiles; S^T = K Q^T on MFMA (key on the
+//             register axis, query on the lane) -> online softmax entirely
+//             lane-local, P stays in registers and feeds P.V as the B operand;
+//             V^T fragments come from ds_read_b64_tr_b16.
+//   backward: phase 1 -- waves own 16-key tiles, sweep queries: S, dP, then
+//             dV^T += dO^T P, dK^T += Q^T dS (accumulator-as-operand, no LDS
+//             round trip). phase 2 -- waves own 16-query tiles, sweep keys:
+//             S^T, dP^T, dQ^T += K^T dS^T. No atomics, deterministic.
+// LDS images (bf16): [rows][HD] with 16-B chunk index XOR-swizzled by f(row)
+// = row&6 (HD=64) or (row>>1)&2 (HD=32): conflict-free for both the
+// ds_read_b128 row reads and the ds_read_b64_tr_b16 transposed reads
+// (checked with tools/lds_bank_sim.py). fp32 parity mode uses padded rows and
+// exact-f32 MFMA (v_mfma_f32_16x16x4_f32).
+// Softmax statistics are kept in log2 units: lse2 = log2(sum 2^(s*scale*log2e)).
+#include "common.h"
+#include "../../include/maeclip.h"
+#include <type_traits>
+
+namespace {
+
+constexpr int NW = 8;            // waves per workgroup
+constexpr int NTH = NW * 64;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;
+
+template <typename T, int HD> struct Img {
+  static constexpr bool BF = sizeof(T) == 2;
+  static constexpr int ROWB = BF ? HD * 2 : HD * 4 + 16;
+  __device__ static __forceinline__ int f(int row) { return HD == 64 ? (row & 6) : ((row >> 1) & 2); }
+  // byte offset of 16-byte chunk c of a row
+  __device__ static __forceinline__ int chunk(int row, int c) {
+    return BF ? row * ROWB + ((c ^ f(row)) << 4) : row * ROWB + (c << 4);
+  }
+  static constexpr int CPR = BF ? HD / 8 : HD / 4;  // 16-B chunks per row
+};
+
+// global [n rows, stride ld] (head slice) -> LDS image, zero rows >= n up to npad
+template <typename T, int HD>
+__device__ __forceinline__ void load_img(char* lds, const T* __restrict__ g, int64_t ld, int n, int npad) {
+  using I = Img<T, HD>;
+  const int total = npad * I::CPR;
+  for (int id = threadIdx.x; id < total; id += NTH) {
+    const int row = id / I::CPR, c = id % I::CPR;
+    v4u v = {0, 0, 0, 0};
+    if (row < n) v = *(const v4u*)(g + (int64_t)row * ld + c * (16 / sizeof(T)));
+    *(v4u*)(lds + I::chunk(row, c)) = v;
+  }
+}
+
+// ---- row fragment: 8 consecutive d (d = 32ks + 8g + j) of LDS row r0 + (lane&15)
+template <typename T, int HD> struct RowFrag;
+template <int HD> struct RowFrag<bf16_t, HD> {
+  v8s v;
+  __device__ __forceinline__ void lds(const char* img, int r0, int ks, int lane) {
+    const int row = r0 + (lane & 15);
+    v = *(const v8s*)(img + Img<bf16_t, HD>::chunk(row, 4 * ks + (lane >> 4)));
+  }
+  __device__ __forceinline__ void glob(const bf16_t* p, int ks, int lane, bool ok) {
+    v = ok ? *(const v8s*)(p + 32 * ks + 8 * (lane >> 4)) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+};
+template <int HD> struct RowFrag<float, HD> {
+  float v[8];
+  __device__ __forceinline__ void lds(const char* img, int r0, int ks, int lane) {
+    const int row = r0 + (lane & 15);
+    const int c0 = 8 * ks + 2 * (lane >> 4);
+    v4f a = *(const v4f*)(img + Img<float, HD>::chunk(row, c0));
+    v4f b = *(const v4f*)(img + Img<float, HD>::chunk(row, c0 + 1));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  }
+  __device__ __forceinline__ void glob(const float* p, int ks, int lane, bool ok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ok ? p[32 * ks + 8 * (lane >> 4) + j] : 0.f;
+  }
+};
+
+// D += X Y over a 32-deep k-step; X, Y row fragments (X rows on lane for A operand).
+__device__ __forceinline__ v4f mma32(const RowFrag<bf16_t, 64>& x, const RowFrag<bf16_t, 64>& y, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.v, y.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ v4f mma32(const RowFrag<bf16_t, 32>& x, const RowFrag<bf16_t, 32>& y, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.v, y.v, c, 0, 0, 0);
+}
+template <int HD>
+__device__ __forceinline__ v4f mma32(const RowFrag<float, HD>& x, const RowFrag<float, HD>& y, v4f c) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(x.v[s], y.v[s], c, 0, 0, 0);
+  return c;
+}
+
+// bf16 transposed fragment: element j <-> row rb + 16*(j>>2) + 4*g + (j&3),
+// column c0 + (lane&15): the A operand "X^T" of a product that sums over rows.
+template <int HD>
+__device__ __forceinline__ v8s tr_frag(const char* img, int rb, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int unit = (c0 >> 2) + p;  // 8-byte unit within the row
+  v8s r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = rb + 16 * h + 4 * g + q;
+    const char* a = img + Img<bf16_t, HD>::chunk(row, unit >> 1) + ((unit & 1) << 3);
+    v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * h + e] = t[e];
+  }
+  return r;
+}
+__device__ __forceinline__ v8s pack_p(const v4f& a, const v4f& b) {
+  v8s r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
+  return r;
+}
+
+// D[c][col] += sum over 32 rows (rb..rb+31) of X[row][c] * P[row][col], where
+// P is held as two accumulator tiles (rows rb+4g+i and rb+16+4g+i on lane col).
+template <typename T, int HD>
+__device__ __forceinline__ v4f mma_rowsum(const char* img, int rb, int c0, const v4f& p0, const v4f& p1,
+                                          v4f acc, int lane) {
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<HD>(img, rb, c0, lane), pack_p(p0, p1), acc, 0, 0, 0);
+  } else {
+    const int g = lane >> 4, col = c0 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x0 = *(const float*)(img + (rb + 4 * g + i) * Img<float, HD>::ROWB + col * 4);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, p0[i], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x1 = *(const float*)(img + (rb + 16 + 4 * g + i) * Img<float, HD>::ROWB + col * 4);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, p1[i], acc, 0, 0, 0);
+    }
+    return acc;
+  }
+}
+
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t bh, int q, int k, uint32_t thr) {
+  return mc_hash4(seed, bh, (uint64_t)q, (uint64_t)k) >= thr;
+}
+
+// ============================================================== forward
+template <typename T, int HD>
+__global__ void __launch_bounds__(NTH) attn_fwd_kernel(const maeclip_attn_args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using I = Img<T, HD>;
+  const int n = a.n, H = a.H;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int npad = (n + 63) & ~63;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  char* Kimg = smem;
+  char* Vimg = smem + npad * I::ROWB;
+  float* kmask = (float*)(smem + 2 * npad * I::ROWB);
+
+  const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  const int HH = H * HD;
+  load_img<T, HD>(Kimg, qkv + HH + h * HD, a.ld_qkv, n, npad);
+  load_img<T, HD>(Vimg, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
+  for (int k = threadIdx.x; k < npad; k += NTH) {
+    float mk = (k < n) ? 0.f : NEG_BIG;
+    if (k < n && a.key_mask && a.key_mask[(int64_t)b * n + k] == 0.f) mk = NEG_BIG;
+    kmask[k] = mk;
+  }
+  __syncthreads();
+
+  const float c = a.scale * LOG2E;
+  const bool drop = a.dropout_p > 0.f;
+  const uint32_t thr = (uint32_t)((double)a.dropout_p * 4294967296.0);
+  const float dscale = drop ? 1.f / (1.f - a.dropout_p) : 1.f;
+  const uint64_t bh = (uint64_t)b * H + h;
+
+  const int nqt = (n + 15) >> 4;
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int q = qt * 16 + (lane & 15);
+    const bool qok = q < n;
+    RowFrag<T, HD> qf[HD / 32];
+#pragma unroll
+    for (int ks = 0; ks < HD / 32; ++ks) qf[ks].glob(qkv + (int64_t)q * a.ld_qkv + h * HD, ks, lane, qok);
+
+    float m = NEG_BIG, lsum = 0.f;
+    v4f o[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < npad; kc += 64) {
+      v4f s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < HD / 32; ++ks) {
+          RowFrag<T, HD> kf;
+          kf.lds(Kimg, kc + 16 * t, ks, lane);
+          s[t] = mma32(kf, qf[ks], s[t]);
+        }
+      }
+      float mloc = NEG_BIG;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kc + 16 * t + 4 * g + i;
+          const float x = s[t][i] * c + kmask[key];
+          s[t][i] = x;
+          mloc = fmaxf(mloc, x);
+        }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float mnew = fmaxf(m, mloc);
+      const float alpha = exp2f(m - mnew);
+      float lp = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(s[t][i] - mnew);
+          lp += p;
+          s[t][i] = p;
+        }
+      lsum = lsum * alpha + lp;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
+      m = mnew;
+      if (drop) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = kc + 16 * t + 4 * g + i;
+            s[t][i] = dropout_keep(a.seed, bh, q, key, thr) ? s[t][i] * dscale : 0.f;
+          }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+          o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const float inv = 1.f / lsum;
+    if (qok) {
+      T* orow = (T*)a.o + ((int64_t)b * n + q) * a.ld_o + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) st4<T>(orow + 16 * dt + 4 * g, o[dt] * inv);
+      if (g == 0 && a.lse) a.lse[((int64_t)b * H + h) * n + q] = m + log2f(lsum);
+    }
+  }
+}
+
+// ============================================================== backward
+template <typename T, int HD>
+__global__ void __launch_bounds__(NTH) attn_bwd_kernel(const maeclip_attn_args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  using I = Img<T, HD>;
+  const int n = a.n, H = a.H;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int npad = (n + 31) & ~31;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int img = npad * I::ROWB;
+  char* Qi = smem;
+  char* Ki = smem + img;
+  char* Vi = smem + 2 * img;
+  char* Di = smem + 3 * img;
+  float* L2 = (float*)(smem + 4 * img);
+  float* Dv = L2 + npad;
+  float* cs = Dv + npad;  // [NW][3*HD] bias-grad partials
+
+  const int HH = H * HD;
+  const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  const T* O = (const T*)a.o + (int64_t)b * n * a.ld_o + h * HD;
+  const T* dO = (const T*)a.dout + (int64_t)b * n * a.ld_o + h * HD;
+  load_img<T, HD>(Qi, qkv + h * HD, a.ld_qkv, n, npad);
+  load_img<T, HD>(Ki, qkv + HH + h * HD, a.ld_qkv, n, npad);
+  load_img<T, HD>(Vi, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
+  load_img<T, HD>(Di, dO, a.ld_o, n, npad);
+  // Dv[q] = rowsum(dO * O); one wave per row, fp32
+  for (int q = wave; q < npad; q += NW) {
+    float acc = 0.f;
+    if (q < n)
+      for (int d = lane; d < HD; d += 64)
+        acc += ld_as_f<T>(O + (int64_t)q * a.ld_o + d) * ld_as_f<T>(dO + (int64_t)q * a.ld_o + d);
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      Dv[q] = acc;
+      L2[q] = q < n ? a.lse[((int64_t)b * H + h) * n + q] : 3.0e38f;
+    }
+  }
+  for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) cs[i] = 0.f;
+  __syncthreads();
+
+  const float c = a.scale * LOG2E;
+  T* dqkv = (T*)a.dqkv + (int64_t)b * n * a.ld_dqkv;
+
+  // ---------------- phase 1: dK, dV (wave owns 16-key tiles)
+  const int nkt = (n + 15) >> 4;
+  for (int kt = wave; kt < nkt; kt += NW) {
+    const int k0 = kt * 16;
+    const int key = k0 + (lane & 15);
+    const bool kok = key < n;
+    RowFrag<T, HD> kf[HD / 32], vf[HD / 32];
+#pragma unroll
+    for (int ks = 0; ks < HD / 32; ++ks) {
+      kf[ks].lds(Ki, k0, ks, lane);
+      vf[ks].lds(Vi, k0, ks, lane);
+    }
+    v4f dv[HD / 16], dk[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) { dv[dt] = v4f{0, 0, 0, 0}; dk[dt] = v4f{0, 0, 0, 0}; }
+
+    for (int qc = 0; qc < npad; qc += 32) {
+      v4f P[2], dS[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q0 = qc + 16 * u;
+        v4f s = {0, 0, 0, 0}, dp = {0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < HD / 32; ++ks) {
+          RowFrag<T, HD> qf, df;
+          qf.lds(Qi, q0, ks, lane);
+          df.lds(Di, q0, ks, lane);
+          s = mma32(qf, kf[ks], s);    // S[q=4g+i][key=lane&15]
+          dp = mma32(df, vf[ks], dp);  // dP[q][key]
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = q0 + 4 * g + i;
+          const float p = kok ? exp2f(s[i] * c - L2[qq]) : 0.f;
+          P[u][i] = p;
+          dS[u][i] = p * (dp[i] - Dv[qq]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        dv[dt] = mma_rowsum<T, HD>(Di, qc, 16 * dt, P[0], P[1], dv[dt], lane);
+        dk[dt] = mma_rowsum<T, HD>(Qi, qc, 16 * dt, dS[0], dS[1], dk[dt], lane);
+      }
+    }
+    // lane holds dV[key][16dt+4g+i], dK likewise
+    if (kok) {
+      T* rowp = dqkv + (int64_t)key * a.ld_dqkv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) {
+        st4<T>(rowp + HH + 16 * dt + 4 * g, dk[dt] * a.scale);
+        st4<T>(rowp + 2 * HH + 16 * dt + 4 * g, dv[dt]);
+      }
+    }
+    if (a.colsum_partial) {
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float sk = kok ? dk[dt][i] * a.scale : 0.f, sv = kok ? dv[dt][i] : 0.f;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            sk += __shfl_xor(sk, o, 64);
+            sv += __shfl_xor(sv, o, 64);
+          }
+          if ((lane & 15) == 0) {
+            cs[wave * 3 * HD + HD + 16 * dt + 4 * g + i] += sk;
+            cs[wave * 3 * HD + 2 * HD + 16 * dt + 4 * g + i] += sv;
+          }
+        }
+    }
+  }
+
+  // ---------------- phase 2: dQ (wave owns 16-query tiles)
+  for (int qt = wave; qt < nkt; qt += NW) {
+    const int q0 = qt * 16;
+    const int q = q0 + (lane & 15);
+    const bool qok = q < n;
+    RowFrag<T, HD> qf[HD / 32], df[HD / 32];
+#pragma unroll
+    for (int ks = 0; ks < HD / 32; ++ks) {
+      qf[ks].lds(Qi, q0, ks, lane);
+      df[ks].lds(Di, q0, ks, lane);
+    }
+    const float lq = L2[q], dq_ = Dv[q];
+    v4f dq[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0, 0, 0, 0};
+    for (int kc = 0; kc < npad; kc += 32) {
+      v4f dST[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kb = kc + 16 * u;
+        v4f s = {0, 0, 0, 0}, dp = {0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < HD / 32; ++ks) {
+          RowFrag<T, HD> kf, vf;
+          kf.lds(Ki, kb, ks, lane);
+          vf.lds(Vi, kb, ks, lane);
+          s = mma32(kf, qf[ks], s);    // S^T[key=4g+i][q=lane&15]
+          dp = mma32(vf, df[ks], dp);  // dP^T
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kk = kb + 4 * g + i;
+          const float p = (kk < n) ? exp2f(s[i] * c - lq) : 0.f;
+          dST[u][i] = p * (dp[i] - dq_);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mma_rowsum<T, HD>(Ki, kc, 16 * dt, dST[0], dST[1], dq[dt], lane);
+    }
+    if (qok) {
+      T* rowp = dqkv + (int64_t)q * a.ld_dqkv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt) st4<T>(rowp + 16 * dt + 4 * g, dq[dt] * a.scale);
+    }
+    if (a.colsum_partial) {
+#pragma unroll
+      for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float sq = qok ? dq[dt][i] * a.scale : 0.f;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) sq += __shfl_xor(sq, o, 64);
+          if ((lane & 15) == 0) cs[wave * 3 * HD + 16 * dt + 4 * g + i] += sq;
+        }
+    }
+  }
+  if (a.colsum_partial) {
+    __syncthreads();
+    // colsum_partial row b: [3*H*HD], this head's q/k/v column slices
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += cs[w * 3 * HD + i];
+      const int part = i / HD, d = i % HD;
+      a.colsum_partial[(int64_t)b * 3 * HH + part * HH + h * HD + d] = s;
+    }
+  }
+}
+
+template <typename T, int HD> size_t fwd_lds(int n) {
+  const int npad = (n + 63) & ~63;
+  return (size_t)2 * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
+}
+template <typename T, int HD> size_t bwd_lds(int n) {
+  const int npad = (n + 31) & ~31;
+  return (size_t)4 * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)NW * 3 * HD * 4;
+}
+
+template <typename T, int HD>
+int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
+  const size_t lds = bwd ? bwd_lds<T, HD>(a.n) : fwd_lds<T, HD>(a.n);
+  MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
+  dim3 grid((unsigned)(a.B * a.H));
+  if (bwd) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((attn_bwd_kernel<T, HD>), grid, dim3(NTH), lds, s, a);
+  } else {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(NTH), lds, s, a);
+  }
+  MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");
+  return 0;
+}
+
+int check(const maeclip_attn_args* a, bool bwd) {
+  MC_CHECK_ARG(a && a->qkv && a->o, "maeclip_attn: null pointer");
+  MC_CHECK_ARG(a->head_dim == 32 || a->head_dim == 64, "maeclip_attn: head_dim must be 32 or 64 (got %d)", a->head_dim);
+  MC_CHECK_ARG(a->B > 0 && a->n > 0 && a->H > 0, "maeclip_attn: bad sizes");
+  MC_CHECK_ARG(a->dtype == MAECLIP_F32 || a->dtype == MAECLIP_BF16, "maeclip_attn: bad dtype");
+  const int epc = a->dtype == MAECLIP_BF16 ? 8 : 4;
+  MC_CHECK_ARG(a->ld_qkv % epc == 0 && a->ld_o % epc == 0, "maeclip_attn: row strides must be 16-byte multiples");
+  if (bwd) {
+    MC_CHECK_ARG(a->dout && a->dqkv && a->lse, "maeclip_attn_bwd: null pointer");
+    MC_CHECK_ARG(a->ld_dqkv % epc == 0, "maeclip_attn_bwd: ld_dqkv");
+  }
+  return 0;
+}
+
+int dispatch(const maeclip_attn_args* a, bool bwd, void* stream) {
+  if (int e = check(a, bwd)) return e;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dtype == MAECLIP_BF16)
+    return a->head_dim == 64 ? run<bf16_t, 64>(*a, bwd, s) : run<bf16_t, 32>(*a, bwd, s);
+  return a->head_dim == 64 ? run<float, 64>(*a, bwd, s) : run<float, 32>(*a, bwd, s);
+}
+
+}  // namespace
+
+extern "C" int32_t maeclip_attn_fwd(const maeclip_attn_args* a, void* stream) { return dispatch(a, false, stream); }
+extern "C" int32_t maeclip_attn_bwd(const maeclip_attn_args* a, void* stream) { return dispatch(a, true, stream); }

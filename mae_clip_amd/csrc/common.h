@@ -1,0 +1,129 @@
+// Shared device/host helpers for libmaeclip (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this library:
+//   * bf16 tensors are passed as raw uint16 bit patterns (bf16_t); fp32 as float.
+//   * Every entry point receives the caller's hipStream_t and never allocates:
+//     workspaces are carved by the Python host from the torch caching allocator.
+//   * Errors are reported through a negative return code plus a thread-local
+//     message (maeclip_last_error), mirroring torch's RuntimeError convention
+//     that the reference's main.py relies on (main.py:54-66 has no handling).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+typedef uint16_t bf16_t;
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+#define MAECLIP_F32 0
+#define MAECLIP_BF16 1
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// ---------------------------------------------------------------- host errors
+namespace maeclip {
+void set_error(const char* fmt, ...);
+}
+
+#define MC_CHECK_ARG(cond, ...)                  \
+  do {                                           \
+    if (!(cond)) {                               \
+      maeclip::set_error(__VA_ARGS__);           \
+      return -1;                                 \
+    }                                            \
+  } while (0)
+
+#define MC_CHECK_LAUNCH(name)                                                   \
+  do {                                                                          \
+    hipError_t _e = hipGetLastError();                                          \
+    if (_e != hipSuccess) {                                                     \
+      maeclip::set_error("%s: launch failed: %s", name, hipGetErrorString(_e)); \
+      return -2;                                                                \
+    }                                                                           \
+  } while (0)
+
+// ------------------------------------------------------------- device helpers
+__device__ __forceinline__ float bf2f(bf16_t u) {
+  return __uint_as_float(((unsigned)u) << 16);
+}
+// Round-to-nearest-even; NaN stays NaN (hipcc lowers the cast to v_cvt_pk_bf16_f32).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+__device__ __forceinline__ unsigned pack2bf(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+template <typename T> __device__ __forceinline__ float ld_as_f(const T* p);
+template <> __device__ __forceinline__ float ld_as_f<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_as_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+
+template <typename T> __device__ __forceinline__ void st_from_f(T* p, float v);
+template <> __device__ __forceinline__ void st_from_f<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st_from_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// 4 consecutive elements <-> float4 (vectorised: 16 B for f32, 8 B for bf16)
+template <typename T> __device__ __forceinline__ v4f ld4(const T* p);
+template <> __device__ __forceinline__ v4f ld4<float>(const float* p) { return *(const v4f*)p; }
+template <> __device__ __forceinline__ v4f ld4<bf16_t>(const bf16_t* p) {
+  v2u u = *(const v2u*)p;
+  v4f r;
+  r[0] = __uint_as_float(u[0] << 16);
+  r[1] = __uint_as_float(u[0] & 0xffff0000u);
+  r[2] = __uint_as_float(u[1] << 16);
+  r[3] = __uint_as_float(u[1] & 0xffff0000u);
+  return r;
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, v4f v);
+template <> __device__ __forceinline__ void st4<float>(float* p, v4f v) { *(v4f*)p = v; }
+template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, v4f v) {
+  v2u u;
+  u[0] = pack2bf(v[0], v[1]);
+  u[1] = pack2bf(v[2], v[3]);
+  *(v2u*)p = u;
+}
+
+// exact (erf) GELU, as nn.GELU() / HF "gelu" / timm default
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based hash used for dropout keep-masks and MAE mask noise.
+// splitmix64 finaliser; restated bit-exactly in oracle/maskrng.py.
+__host__ __device__ __forceinline__ uint64_t mc_mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint32_t mc_hash4(uint64_t seed, uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t h = mc_mix64(seed);
+  h = mc_mix64(h ^ a);
+  h = mc_mix64(h ^ b);
+  h = mc_mix64(h ^ c);
+  return (uint32_t)(h >> 32);
+}

@@ -1,0 +1,293 @@
+// HBM-bound helper kernels: deterministic column reductions (bias/LN-param
+// gradients), timm global_pool="avg" (modules.py:17-19 -> VisionTransformer
+// forward_head), dropout masks, DistilBERT embedding gather, multi-tensor
+// fp32->bf16 weight casts and the fused multi-tensor AdamW step that replaces
+// torch.optim.AdamW (main.py:101-103,59).
+#include "common.h"
+#include "../../include/maeclip.h"
+
+namespace {
+constexpr int NTH = 256;
+
+// out[n] (+)= sum_p partial[p][n]  -- fixed summation order, vectorised over n
+__global__ void __launch_bounds__(NTH) colsum_reduce_kernel(const float* __restrict__ part, int64_t P, int64_t N,
+                                                            float* __restrict__ out, int accumulate, float scale) {
+  const int64_t n = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  if (n >= N) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int64_t p = 0;
+  for (; p + 3 < P; p += 4) {
+    s0 += part[(p + 0) * N + n];
+    s1 += part[(p + 1) * N + n];
+    s2 += part[(p + 2) * N + n];
+    s3 += part[(p + 3) * N + n];
+  }
+  for (; p < P; ++p) s0 += part[p * N + n];
+  const float s = ((s0 + s1) + (s2 + s3)) * scale;
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+// single-vector sum (P large, N == 1): one workgroup, fixed-order tree
+__global__ void __launch_bounds__(NTH) vec_sum_kernel(const float* __restrict__ x, int64_t P, float* __restrict__ out,
+                                                      int accumulate, float scale) {
+  __shared__ float red[NTH / 64];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < P; i += NTH) s += x[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < NTH / 64; ++w) t += red[w];
+    t *= scale;
+    out[0] = accumulate ? out[0] + t : t;
+  }
+}
+
+// feat[b] = mean_{t=1..n-1} x[b,t,:]   (timm global_pool="avg", num_prefix_tokens=1)
+__global__ void __launch_bounds__(NTH) pool_fwd_kernel(const float* __restrict__ x, int n, int D, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int d = blockIdx.x * NTH + threadIdx.x;
+  if (d >= D) return;
+  const float* p = x + (int64_t)b * n * D + d;
+  float s = 0.f;
+  for (int t = 1; t < n; ++t) s += p[(int64_t)t * D];
+  out[(int64_t)b * D + d] = s / (float)(n - 1);
+}
+__global__ void __launch_bounds__(NTH) pool_bwd_kernel(const float* __restrict__ dout, int n, int D, float* __restrict__ dx,
+                                                       int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  const int64_t total = (int64_t)gridDim.y * n * D;
+  (void)total;
+  const int b = blockIdx.y;
+  if (i >= (int64_t)n * D) return;
+  const int t = (int)(i / D), d = (int)(i % D);
+  const float v = t == 0 ? 0.f : dout[(int64_t)b * D + d] / (float)(n - 1);
+  float* o = dx + (int64_t)b * n * D + i;
+  *o = accumulate ? *o + v : v;
+}
+
+// y = x * keep/(1-p) with the same mask function as the LayerNorm input dropout
+__global__ void __launch_bounds__(NTH) dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t M, int D,
+                                                      int64_t ld, float p, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  if (i >= M * D) return;
+  const int64_t r = i / D;
+  const int c = (int)(i % D);
+  const uint32_t thr = (uint32_t)((double)p * 4294967296.0);
+  const float k = mc_hash4(seed, (uint64_t)r, (uint64_t)c, 0x4c4eull) >= thr ? 1.f / (1.f - p) : 0.f;
+  y[r * ld + c] = x[r * ld + c] * k;
+}
+
+// DistilBERT Embeddings (modeling_distilbert.py:92-117) up to the LayerNorm:
+// out[b*T+t] = word[ids[b,t]] + pos[t]
+__global__ void __launch_bounds__(NTH) embed_kernel(const int64_t* __restrict__ ids, const float* __restrict__ word,
+                                                    const float* __restrict__ pos, int T, int D, int64_t V,
+                                                    float* __restrict__ out) {
+  const int64_t row = blockIdx.y;
+  const int d = (blockIdx.x * NTH + threadIdx.x) * 4;
+  if (d >= D) return;
+  int64_t id = ids[row];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const int t = (int)(row % T);
+  v4f w = *(const v4f*)(word + id * D + d);
+  v4f pp = *(const v4f*)(pos + (int64_t)t * D + d);
+  *(v4f*)(out + row * D + d) = w + pp;
+}
+
+
+// colsum partials of a row matrix (bias gradient of a Linear whose output
+// gradient arrives un-reduced), optionally emitting a bf16 copy of the rows.
+constexpr int RC_MAXC = 8;  // D <= 2048
+template <typename T>
+__global__ void __launch_bounds__(NTH) rows_colsum_kernel(const T* __restrict__ x, int64_t M, int D, int64_t ld,
+                                                          bf16_t* __restrict__ out_bf, float* __restrict__ partial) {
+  __shared__ float red[NTH / 64][RC_MAXC * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc[RC_MAXC][4];
+#pragma unroll
+  for (int c = 0; c < RC_MAXC; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * (NTH / 64) + wave; r < M; r += (int64_t)gridDim.x * (NTH / 64)) {
+#pragma unroll
+    for (int c = 0; c < RC_MAXC; ++c) {
+      const int e = c * 256 + lane * 4;
+      if (e < D) {
+        const v4f v = ld4<T>(x + r * ld + e);
+        acc[c][0] += v[0]; acc[c][1] += v[1]; acc[c][2] += v[2]; acc[c][3] += v[3];
+        if (out_bf) st4<bf16_t>(out_bf + r * D + e, v);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < RC_MAXC; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = c * 256 + lane * 4 + j;
+      if (e < D) red[wave][e] = acc[c][j];
+    }
+  __syncthreads();
+  for (int e = threadIdx.x; e < D; e += NTH) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NTH / 64; ++k) s += red[k][e];
+    partial[(int64_t)blockIdx.x * D + e] = s;
+  }
+}
+int rows_colsum_grid(int64_t M) {
+  const int64_t g = (M + 3) / 4;
+  return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
+}
+
+// ---- multi-tensor: one block per CHUNK elements, entries located by binary search
+constexpr int64_t CHUNK = 4096;
+
+__device__ __forceinline__ int find_entry(const maeclip_mt_entry* e, int ne, int64_t blk) {
+  int lo = 0, hi = ne - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (e[mid].chunk_start <= blk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(NTH) cast_multi_kernel(const maeclip_mt_entry* __restrict__ e, int ne) {
+  const int k = find_entry(e, ne, blockIdx.x);
+  const int64_t base = (blockIdx.x - e[k].chunk_start) * CHUNK;
+  const float* src = (const float*)e[k].p0;
+  bf16_t* dst = (bf16_t*)e[k].p4;
+  const int64_t n = e[k].n;
+  for (int64_t i = base + threadIdx.x * 4; i < base + CHUNK && i < n; i += NTH * 4) {
+    if (i + 3 < n) {
+      st4<bf16_t>(dst + i, *(const v4f*)(src + i));
+    } else {
+      for (int64_t j = i; j < n; ++j) dst[j] = f2bf(src[j]);
+    }
+  }
+}
+
+// torch.optim.AdamW (decoupled weight decay), torch/optim/adamw.py _single_tensor_adamw:
+//   p *= 1 - lr*wd ; m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void __launch_bounds__(NTH) adamw_multi_kernel(const maeclip_mt_entry* __restrict__ e, int ne,
+                                                          maeclip_adamw_hparams hp) {
+  const int k = find_entry(e, ne, blockIdx.x);
+  const int64_t base = (blockIdx.x - e[k].chunk_start) * CHUNK;
+  float* p = (float*)e[k].p0;
+  const float* gr = (const float*)e[k].p1;
+  float* m = (float*)e[k].p2;
+  float* v = (float*)e[k].p3;
+  bf16_t* sh = (bf16_t*)e[k].p4;
+  const int64_t n = e[k].n;
+  const float decay = 1.f - hp.lr * hp.weight_decay;
+  const float b1 = hp.beta1, b2 = hp.beta2;
+  for (int64_t i = base + threadIdx.x; i < base + CHUNK && i < n; i += NTH) {
+    const float g = gr[i] * hp.grad_scale;
+    float pi = p[i] * decay;
+    const float mi = b1 * m[i] + (1.f - b1) * g;
+    const float vi = b2 * v[i] + (1.f - b2) * g * g;
+    const float denom = sqrtf(vi) / hp.bc2_sqrt + hp.eps;
+    pi -= hp.step_size * mi / denom;
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+    if (sh) sh[i] = f2bf(pi);
+  }
+}
+
+int64_t mt_blocks(const maeclip_mt_entry* host_entries, int ne) {
+  if (ne <= 0) return 0;
+  return host_entries[ne - 1].chunk_start + (host_entries[ne - 1].n + CHUNK - 1) / CHUNK;
+}
+
+}  // namespace
+
+extern "C" int64_t maeclip_mt_chunk(void) { return CHUNK; }
+
+extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate,
+                                         float scale, void* stream) {
+  MC_CHECK_ARG(partial && out && P >= 1 && N >= 1, "maeclip_colsum_reduce: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  if (N == 1) {
+    hipLaunchKernelGGL(vec_sum_kernel, dim3(1), dim3(NTH), 0, s, partial, P, out, accumulate, scale);
+  } else {
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + NTH - 1) / NTH)), dim3(NTH), 0, s, partial, P, N, out,
+                       accumulate, scale);
+  }
+  MC_CHECK_LAUNCH("maeclip_colsum_reduce");
+  return 0;
+}
+
+
+extern "C" int32_t maeclip_rows_colsum_partial_rows(int64_t M) { return rows_colsum_grid(M); }
+
+extern "C" int32_t maeclip_rows_colsum(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld, void* out_bf16,
+                                       float* partial, void* stream) {
+  MC_CHECK_ARG(x && partial && M >= 1 && D > 0 && D <= RC_MAXC * 256 && D % 4 == 0 && ld % 4 == 0,
+               "maeclip_rows_colsum: bad args");
+  dim3 grid((unsigned)rows_colsum_grid(M));
+  if (dtype == MAECLIP_BF16)
+    hipLaunchKernelGGL((rows_colsum_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, (const bf16_t*)x, M, (int)D,
+                       ld, (bf16_t*)out_bf16, partial);
+  else
+    hipLaunchKernelGGL((rows_colsum_kernel<float>), grid, dim3(NTH), 0, (hipStream_t)stream, (const float*)x, M, (int)D, ld,
+                       (bf16_t*)out_bf16, partial);
+  MC_CHECK_LAUNCH("maeclip_rows_colsum");
+  return 0;
+}
+
+extern "C" int32_t maeclip_pool_fwd(const float* x, int32_t B, int32_t n, int32_t D, float* out, void* stream) {
+  MC_CHECK_ARG(x && out && B > 0 && n > 1 && D > 0, "maeclip_pool_fwd: bad args");
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3((D + NTH - 1) / NTH, B), dim3(NTH), 0, (hipStream_t)stream, x, n, D, out);
+  MC_CHECK_LAUNCH("maeclip_pool_fwd");
+  return 0;
+}
+
+extern "C" int32_t maeclip_pool_bwd(const float* dout, int32_t B, int32_t n, int32_t D, float* dx, int32_t accumulate,
+                                    void* stream) {
+  MC_CHECK_ARG(dout && dx && B > 0 && n > 1 && D > 0, "maeclip_pool_bwd: bad args");
+  const int64_t per = (int64_t)n * D;
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)((per + NTH - 1) / NTH), B), dim3(NTH), 0, (hipStream_t)stream, dout,
+                     n, D, dx, accumulate);
+  MC_CHECK_LAUNCH("maeclip_pool_bwd");
+  return 0;
+}
+
+extern "C" int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed,
+                                   void* stream) {
+  MC_CHECK_ARG(x && y && M >= 0 && D > 0 && p >= 0.f && p < 1.f, "maeclip_dropout: bad args");
+  if (M == 0) return 0;
+  const int64_t total = M * D;
+  hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)((total + NTH - 1) / NTH)), dim3(NTH), 0, (hipStream_t)stream, x, y, M,
+                     D, ld, p, seed);
+  MC_CHECK_LAUNCH("maeclip_dropout");
+  return 0;
+}
+
+extern "C" int32_t maeclip_embed_fwd(const int64_t* ids, const float* word, const float* pos, int32_t B, int32_t T,
+                                     int32_t D, int64_t V, float* out, void* stream) {
+  MC_CHECK_ARG(ids && word && pos && out && D % 4 == 0, "maeclip_embed_fwd: bad args");
+  hipLaunchKernelGGL(embed_kernel, dim3((D / 4 + NTH - 1) / NTH, (unsigned)(B * T)), dim3(NTH), 0, (hipStream_t)stream, ids,
+                     word, pos, T, D, V, out);
+  MC_CHECK_LAUNCH("maeclip_embed_fwd");
+  return 0;
+}
+
+extern "C" int32_t maeclip_cast_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries, int32_t ne,
+                                      void* stream) {
+  MC_CHECK_ARG(dev_entries && host_entries && ne > 0, "maeclip_cast_multi: bad args");
+  const int64_t nb = mt_blocks(host_entries, ne);
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(cast_multi_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, dev_entries, ne);
+  MC_CHECK_LAUNCH("maeclip_cast_multi");
+  return 0;
+}
+
+extern "C" int32_t maeclip_adamw_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries,
+                                       int32_t ne, const maeclip_adamw_hparams* hp, void* stream) {
+  MC_CHECK_ARG(dev_entries && host_entries && hp && ne > 0, "maeclip_adamw_multi: bad args");
+  const int64_t nb = mt_blocks(host_entries, ne);
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(adamw_multi_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, dev_entries, ne, *hp);
+  MC_CHECK_LAUNCH("maeclip_adamw_multi");
+  return 0;
+}

@@ -1,0 +1,221 @@
+// LayerNorm forward/backward, one wave per row (gfx950).
+//
+// Replaces nn.LayerNorm at every site of the hot path: timm Block norm1/norm2
+// and fc_norm (eps 1e-6), ProjectionHead.layer_norm (modules.py:67, eps 1e-5),
+// HF ViTMAE decoder layernorms (eps 1e-6 after config), DistilBERT
+// Embeddings.LayerNorm / sa_layer_norm / output_layer_norm (eps 1e-12,
+// modeling_distilbert.py:88,236,239).
+//
+// Fusions (each saves a full HBM pass over an [M,D] activation):
+//   fwd: x' = dropout(x) + res       (post-LN residual of DistilBERT, ProjectionHead)
+//        y  = LN(x') [+ dropout]     (Embeddings dropout after LN)
+//        y2 = bf16 copy of y         (GEMM operand) ; x' saved for backward
+//   bwd: dx = LN'(dy) + dres         (pre-LN residual stream gradient)
+//        dx_bf = bf16 copy of dx     (next GEMM operand)
+//        per-block partials of dgamma, dbeta and colsum(dx) (= the bias gradient
+//        of the Linear that produced the residual branch), reduced by
+//        maeclip_colsum_reduce -> deterministic.
+// Statistics are fp32 two-pass (mean, then sum of squared deviations), as torch.
+#include "common.h"
+#include "../../include/maeclip.h"
+
+namespace {
+
+constexpr int NTH = 256;
+constexpr int MAXC = 8;  // chunks of 4 elements per lane -> D <= 2048
+
+template <typename T>
+__device__ __forceinline__ void load_row(float (&v)[MAXC][4], const T* p, int D, int lane) {
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int e = c * 256 + lane * 4;
+    if (e < D) {
+      v4f t = ld4<T>(p + e);
+      v[c][0] = t[0]; v[c][1] = t[1]; v[c][2] = t[2]; v[c][3] = t[3];
+    } else {
+      v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ float keepf(uint64_t seed, int64_t row, int col, uint32_t thr, float sc) {
+  return mc_hash4(seed, (uint64_t)row, (uint64_t)col, 0x4c4eull) >= thr ? sc : 0.f;
+}
+
+template <typename XT, typename YT>
+__global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (NTH / 64) + (threadIdx.x >> 6);
+  if (row >= a.M) return;
+  const int D = (int)a.D;
+  float v[MAXC][4];
+  load_row<XT>(v, (const XT*)a.x + row * a.ldx, D, lane);
+  if (a.in_dropout_p > 0.f) {
+    const uint32_t thr = (uint32_t)((double)a.in_dropout_p * 4294967296.0);
+    const float sc = 1.f / (1.f - a.in_dropout_p);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[c][j] *= keepf(a.seed_in, row, c * 256 + lane * 4 + j, thr, sc);
+  }
+  if (a.res) {
+    float r[MAXC][4];
+    load_row<float>(r, a.res + row * a.ldres, D, lane);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[c][j] += r[c][j];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[c][j];
+  const float mean = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c * 256 + lane * 4 < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[c][j] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / D + a.eps);
+  if (lane == 0) {
+    if (a.mean) a.mean[row] = mean;
+    if (a.rstd) a.rstd[row] = rstd;
+  }
+  const bool odrop = a.out_dropout_p > 0.f;
+  const uint32_t othr = (uint32_t)((double)a.out_dropout_p * 4294967296.0);
+  const float osc = odrop ? 1.f / (1.f - a.out_dropout_p) : 1.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int e = c * 256 + lane * 4;
+    if (e >= D) continue;
+    if (a.xsum_out) *(v4f*)(a.xsum_out + row * a.ldxs + e) = v4f{v[c][0], v[c][1], v[c][2], v[c][3]};
+    const v4f gm = *(const v4f*)(a.gamma + e);
+    const v4f bt = *(const v4f*)(a.beta + e);
+    v4f y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      y[j] = (v[c][j] - mean) * rstd * gm[j] + bt[j];
+      if (odrop) y[j] *= keepf(a.seed_out, row, e + j, othr, osc);
+    }
+    st4<YT>((YT*)a.y + row * a.ldy + e, y);
+    if (a.y2) st4<bf16_t>((bf16_t*)a.y2 + row * a.ldy2 + e, y);
+  }
+}
+
+template <typename GT, typename XT>
+__global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a) {
+  __shared__ float red[NTH / 64][MAXC * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int D = (int)a.D;
+  float pg[MAXC][4], pb[MAXC][4], pc[MAXC][4];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pg[c][j] = pb[c][j] = pc[c][j] = 0.f;
+
+  float gm[MAXC][4];
+  load_row<float>(gm, a.gamma, D, lane);
+
+  for (int64_t row = (int64_t)blockIdx.x * (NTH / 64) + wave; row < a.M; row += (int64_t)gridDim.x * (NTH / 64)) {
+    float dy[MAXC][4], x[MAXC][4];
+    load_row<GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
+    load_row<XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (x[c][j] - mean) * rstd;
+        x[c][j] = xh;
+        const float gdy = dy[c][j] * gm[c][j];
+        s1 += gdy;
+        s2 += gdy * xh;
+        pg[c][j] += dy[c][j] * xh;
+        pb[c][j] += dy[c][j];
+      }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    float dr[MAXC][4];
+    if (a.dres) load_row<float>(dr, a.dres + row * a.lddx, D, lane);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int e = c * 256 + lane * 4;
+      if (e >= D) continue;
+      v4f o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float d = rstd * (dy[c][j] * gm[c][j] - s1 - x[c][j] * s2);
+        if (a.dres) d += dr[c][j];
+        o[j] = d;
+        pc[c][j] += d;
+      }
+      *(v4f*)(a.dx + row * a.lddx + e) = o;
+      if (a.dx_bf) st4<bf16_t>((bf16_t*)a.dx_bf + row * a.lddx_bf + e, o);
+    }
+  }
+  // cross-wave reduction of the three per-lane partial vectors
+  float* outs[3] = {a.dgamma_partial, a.dbeta_partial, a.dx_colsum_partial};
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    if (!outs[w]) continue;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = c * 256 + lane * 4 + j;
+        if (e < D) red[wave][e] = (w == 0 ? pg[c][j] : (w == 1 ? pb[c][j] : pc[c][j]));
+      }
+    __syncthreads();
+    for (int e = threadIdx.x; e < D; e += NTH) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < NTH / 64; ++k) s += red[k][e];
+      outs[w][(int64_t)blockIdx.x * D + e] = s;
+    }
+    __syncthreads();
+  }
+}
+
+int ln_bwd_grid(int64_t M) {
+  int64_t g = (M + 3) / 4;
+  return (int)(g < 1024 ? g : 1024);
+}
+
+}  // namespace
+
+extern "C" int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* a, void* stream) {
+  MC_CHECK_ARG(a && a->x && a->y && a->gamma && a->beta, "maeclip_ln_fwd: null pointer");
+  MC_CHECK_ARG(a->D > 0 && a->D <= MAXC * 256 && a->D % 4 == 0, "maeclip_ln_fwd: D=%lld unsupported", (long long)a->D);
+  if (a->M == 0) return 0;
+  dim3 grid((unsigned)((a->M + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  const bool xb = a->x_dtype == MAECLIP_BF16, yb = a->y_dtype == MAECLIP_BF16;
+  if (xb && yb) hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);
+  else if (xb) hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, float>), grid, dim3(NTH), 0, s, *a);
+  else if (yb) hipLaunchKernelGGL((ln_fwd_kernel<float, bf16_t>), grid, dim3(NTH), 0, s, *a);
+  else hipLaunchKernelGGL((ln_fwd_kernel<float, float>), grid, dim3(NTH), 0, s, *a);
+  MC_CHECK_LAUNCH("maeclip_ln_fwd");
+  return 0;
+}
+
+extern "C" int32_t maeclip_ln_bwd_partial_rows(int64_t M) { return ln_bwd_grid(M); }
+
+extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
+  MC_CHECK_ARG(a && a->dy && a->x && a->mean && a->rstd && a->gamma && a->dx, "maeclip_ln_bwd: null pointer");
+  MC_CHECK_ARG(a->D > 0 && a->D <= MAXC * 256 && a->D % 4 == 0, "maeclip_ln_bwd: D unsupported");
+  if (a->M == 0) return 0;
+  dim3 grid((unsigned)ln_bwd_grid(a->M));
+  hipStream_t s = (hipStream_t)stream;
+  const bool gb = a->dy_dtype == MAECLIP_BF16, xb = a->x_dtype == MAECLIP_BF16;
+  if (gb && xb) hipLaunchKernelGGL((ln_bwd_kernel<bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);
+  else if (gb) hipLaunchKernelGGL((ln_bwd_kernel<bf16_t, float>), grid, dim3(NTH), 0, s, *a);
+  else if (xb) hipLaunchKernelGGL((ln_bwd_kernel<float, bf16_t>), grid, dim3(NTH), 0, s, *a);
+  else hipLaunchKernelGGL((ln_bwd_kernel<float, float>), grid, dim3(NTH), 0, s, *a);
+  MC_CHECK_LAUNCH("maeclip_ln_bwd");
+  return 0;
+}

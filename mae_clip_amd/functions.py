@@ -1,0 +1,338 @@
+"""torch.autograd.Functions of the hot path, each a fixed sequence of
+libmaeclip kernel launches (no torch compute kernels inside).
+
+Granularity follows the fusion boundaries, not nn.Module boundaries: a whole
+pre-LN transformer stack is ONE Function, so the residual-stream gradient, its
+bf16 copy and the bias-gradient column partials flow from block to block
+inside the backward without extra passes over HBM.
+
+Reference ops replaced (file:line):
+  TransformerStackFn  timm Block x depth (modules.py:17-19 -> timm 0.9.12) and
+                      HF ViTMAELayer x decoder_depth (modeling_vit_mae.py:455-580)
+  PatchTokensFn       timm PatchEmbed + _pos_embed (+ MAE visible-patch gather)
+  EncoderHeadFn       timm global_pool="avg" + fc_norm; MAE mae_norm
+  DecoderEmbedFn      HF decoder_embed + mask-token unshuffle + pos (:536-566)
+  MaeHeadLossFn       HF decoder_norm + decoder_pred + loss (:568-578, :852-859)
+  ProjectionHeadFn    modules.py:69-76 (always fp32)
+  ClipLossFn          CLIP.py:34-43
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import kernels as K
+
+
+def _reduce(part):
+    return K.colsum_reduce(part)
+
+
+# ---------------------------------------------------------------- stacks
+@dataclass
+class StackSpec:
+    B: int
+    n: int
+    D: int
+    H: int
+    eps: float
+    dtype: torch.dtype              # compute dtype of GEMM operands / activations
+    wT: list                        # per block: (qkv, proj, fc1, fc2) weights in `dtype`
+
+
+PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
+
+
+class TransformerStackFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, spec: StackSpec, *params):
+        B, n, D, H = spec.B, spec.n, spec.D, spec.H
+        hd = D // H
+        scale = hd ** -0.5
+        T = spec.dtype
+        M = B * n
+        xi = x.reshape(M, D)
+        saved = []
+        for i, (wqkv, wproj, w1, w2) in enumerate(spec.wT):
+            p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
+            n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
+            h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T)
+            qkv = K.linear_fwd(h1, wqkv, bqkv)
+            o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
+            x1 = K.linear_fwd(o, wproj, bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
+            h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T)
+            pre = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
+            a = K.linear_fwd(h2, w1, b1, epilogue=K.EPI_GELU, aux_out=pre)
+            x2 = K.linear_fwd(a, w2, b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
+            saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, pre, a])
+            xi = x2
+        ctx.saved = saved
+        ctx.spec = spec
+        ctx.params = params
+        return xi.view(B, n, D)
+
+    @staticmethod
+    def backward(ctx, gy):
+        spec = ctx.spec
+        B, n, D, H = spec.B, spec.n, spec.D, spec.H
+        hd = D // H
+        scale = hd ** -0.5
+        T = spec.dtype
+        bf = T == torch.bfloat16
+        M = B * n
+        params = ctx.params
+        grads = [None] * len(params)
+        g = gy.reshape(M, D)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        gT = torch.empty((M, D), device=g.device, dtype=torch.bfloat16) if bf else None
+        cpart = K.rows_colsum(g, out_bf16=gT)
+        if not bf:
+            gT = g
+        for i in reversed(range(len(spec.wT))):
+            wqkv, wproj, w1, w2 = spec.wT[i]
+            p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
+            n1w, n2w = p[0], p[6]
+            xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, pre, a = ctx.saved[i]
+            gi = [None] * PER_BLOCK
+            # mlp.fc2 (+ GELU backward fused into the dgrad epilogue)
+            gi[11] = _reduce(cpart)
+            dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
+            dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_DGELU, aux=pre, colsum=dA_part)
+            gi[10] = K.linear_wgrad(gT, a)
+            del a, pre
+            # mlp.fc1
+            gi[9] = _reduce(dA_part)
+            dh2 = K.linear_dgrad(dA, w1)
+            gi[8] = K.linear_wgrad(dA, h2)
+            del dA
+            # norm2 (+ residual gradient)
+            dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True)
+            gi[6], gi[7] = _reduce(pg), _reduce(pb)
+            if not bf:
+                dx1T = dx1
+            # attn.proj
+            gi[5] = _reduce(pc)
+            dO = K.linear_dgrad(dx1T, wproj)
+            gi[4] = K.linear_wgrad(dx1T, o)
+            # attention
+            dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
+            del dO
+            gi[3] = _reduce(qpart)
+            dh1 = K.linear_dgrad(dqkv, wqkv)
+            gi[2] = K.linear_wgrad(dqkv, h1)
+            del dqkv
+            # norm1 (+ residual gradient)
+            dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True)
+            gi[0], gi[1] = _reduce(pg), _reduce(pb)
+            ctx.saved[i] = None
+            g, gT, cpart = dx, (dxT if bf else dx), pc
+            for j in range(PER_BLOCK):
+                grads[i * PER_BLOCK + j] = gi[j].view(p[j].shape)
+        ctx.saved = None
+        return (g.view(B, n, D), None, *grads)
+
+
+# ------------------------------------------------------------ patch embed
+@dataclass
+class PatchSpec:
+    B: int
+    L: int
+    keep: int
+    p: int
+    kpad: int
+    dtype: torch.dtype
+    w_T: torch.Tensor        # [D, kpad] patch-embed weight in `dtype`
+
+
+class PatchTokensFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, ids_shuffle, ids_restore, spec: PatchSpec, w, b, cls, pos):
+        Xp = K.patch_gather(img, ids_shuffle, spec.keep, spec.p, spec.kpad, spec.dtype)
+        Y = K.linear_fwd(Xp, spec.w_T, b, out_dtype=torch.float32)
+        x = K.tokens_fwd(Y, ids_shuffle, pos.view(-1, pos.shape[-1]), cls.view(-1), spec.B, spec.L, spec.keep)
+        ctx.save = (Xp, ids_restore)
+        ctx.spec = spec
+        ctx.wshape = w.shape
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        spec = ctx.spec
+        Xp, ids_restore = ctx.save
+        gx = gx.contiguous()
+        dY, dpos, dcls = K.tokens_bwd(gx, ids_restore, spec.B, spec.L, spec.keep, spec.dtype)
+        dW = K.linear_wgrad(dY, Xp)
+        Kreal = ctx.wshape[1] * ctx.wshape[2] * ctx.wshape[3]
+        if Kreal != spec.kpad:
+            dW = dW[:, :Kreal].contiguous()
+        db = _reduce(K.rows_colsum(dY))
+        D = dpos.shape[-1]
+        return None, None, None, None, dW.view(ctx.wshape), db, dcls.view(1, 1, D), dpos.view(1, -1, D)
+
+
+# ------------------------------------------------------- encoder outputs
+class EncoderHeadFn(torch.autograd.Function):
+    """features = fc_norm(mean_{t>=1} x[:, t]) ; latent = mae_norm(x) (optional)."""
+
+    @staticmethod
+    def forward(ctx, x, latent_dtype, fcn_w, fcn_b, mn_w, mn_b):
+        B, n, D = x.shape
+        pooled = K.pool_fwd(x)
+        feat, fm, fr, _, _ = K.ln_fwd(pooled, fcn_w, fcn_b, 1e-6, out_dtype=torch.float32)
+        ctx.mae = mn_w is not None
+        latent = None
+        if ctx.mae:
+            latent, lm, lr, _, _ = K.ln_fwd(x.view(B * n, D), mn_w, mn_b, 1e-6, out_dtype=latent_dtype)
+            ctx.lstats = (lm, lr)
+        ctx.save = (x, pooled, fm, fr)
+        ctx.w = (fcn_w, mn_w)
+        if latent is None:
+            return feat
+        return feat, latent
+
+    @staticmethod
+    def backward(ctx, gfeat, glatent=None):
+        x, pooled, fm, fr = ctx.save
+        fcn_w, mn_w = ctx.w
+        B, n, D = x.shape
+        dpooled, _, pg, pb, _ = K.ln_bwd(gfeat.contiguous(), pooled, fm, fr, fcn_w)
+        dx = K.pool_bwd(dpooled, n)
+        g_fw, g_fb = _reduce(pg), _reduce(pb)
+        g_mw = g_mb = None
+        if ctx.mae and glatent is not None:
+            lm, lr = ctx.lstats
+            dx2, _, pg2, pb2, _ = K.ln_bwd(glatent.contiguous(), x.view(B * n, D), lm, lr, mn_w,
+                                           dres=dx.view(B * n, D))
+            dx = dx2.view(B, n, D)
+            g_mw, g_mb = _reduce(pg2), _reduce(pb2)
+        return dx, None, g_fw, g_fb, g_mw, g_mb
+
+
+# ------------------------------------------------------------ MAE decoder
+@dataclass
+class DecSpec:
+    B: int
+    L: int
+    keep: int
+    dtype: torch.dtype
+    w_T: torch.Tensor        # decoder_embed weight in dtype
+
+
+class DecoderEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, latent, ids_shuffle, ids_restore, spec: DecSpec, w, b, mask_token, pos):
+        y = K.linear_fwd(latent, spec.w_T, b, out_dtype=torch.float32)
+        xd = K.unshuffle_fwd(y, ids_restore, mask_token.view(-1), pos.view(-1, pos.shape[-1]), spec.B, spec.L,
+                             spec.keep)
+        ctx.save = (latent, ids_shuffle)
+        ctx.spec = spec
+        return xd
+
+    @staticmethod
+    def backward(ctx, gxd):
+        spec = ctx.spec
+        latent, ids_shuffle = ctx.save
+        dy, dmask_part, cs = K.unshuffle_bwd(gxd.contiguous(), ids_shuffle, spec.B, spec.L, spec.keep, spec.dtype)
+        dlatent = K.linear_dgrad(dy, spec.w_T)
+        dW = K.linear_wgrad(dy, latent)
+        db = _reduce(cs)
+        dmask = _reduce(dmask_part)
+        return dlatent, None, None, None, dW, db, dmask.view(1, 1, -1), None
+
+
+@dataclass
+class MaeHeadSpec:
+    p: int
+    norm_pix: bool
+    mask_count: float
+    loss_scale: float
+    dtype: torch.dtype
+    w_T: torch.Tensor        # decoder_pred weight in dtype
+
+
+class MaeHeadLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xd, img, mask, spec: MaeHeadSpec, dn_w, dn_b, wp, bp):
+        B, n, Dd = xd.shape
+        x2 = xd.view(B * n, Dd)
+        h, m, r, _, _ = K.ln_fwd(x2, dn_w, dn_b, 1e-6, out_dtype=spec.dtype)
+        pred = K.linear_fwd(h, spec.w_T, bp)
+        row = K.mae_loss_fwd(pred, img, mask, spec.p, spec.norm_pix)
+        loss = K.colsum_reduce(row.view(-1, 1), scale=1.0 / spec.mask_count).view(())
+        ctx.save = (x2, h, m, r, pred, img, mask)
+        ctx.spec = spec
+        ctx.dn_w = dn_w
+        ctx.shape = xd.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        spec = ctx.spec
+        x2, h, m, r, pred, img, mask = ctx.save
+        dpred, cs = K.mae_loss_bwd(pred, img, mask, spec.p, spec.norm_pix, gl.contiguous(), spec.mask_count,
+                                   spec.loss_scale)
+        dh = K.linear_dgrad(dpred, spec.w_T)
+        dWp = K.linear_wgrad(dpred, h)
+        dbp = _reduce(cs)
+        dx, _, pg, pb, _ = K.ln_bwd(dh, x2, m, r, ctx.dn_w)
+        return dx.view(ctx.shape), None, None, None, _reduce(pg), _reduce(pb), dWp, dbp
+
+
+# --------------------------------------------------------- projection head
+@dataclass
+class ProjSpec:
+    p_drop: float
+    seed: int
+
+
+class ProjectionHeadFn(torch.autograd.Function):
+    """modules.py:69-76 in fp32: z = dropout(fc(gelu(proj(x)))) + proj(x); LN(z)."""
+
+    @staticmethod
+    def forward(ctx, x, spec: ProjSpec, wp, bp, wf, bf, lw, lb):
+        x = x.contiguous() if x.stride(-1) != 1 else x
+        Bn, P = x.shape[0], wp.shape[0]
+        pre = torch.empty((Bn, P), device=x.device, dtype=torch.float32)
+        g = K.linear_fwd(x, wp, bp, epilogue=K.EPI_GELU, aux_out=pre)
+        f = K.linear_fwd(g, wf, bf)
+        out, m, r, _, z = K.ln_fwd(f, lw, lb, 1e-5, out_dtype=torch.float32, res=pre, in_dropout=spec.p_drop,
+                                   seed_in=spec.seed, xsum=True)
+        ctx.save = (x, pre, g, z, m, r)
+        ctx.w = (wp, wf, lw)
+        ctx.spec = spec
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, pre, g, z, m, r = ctx.save
+        wp, wf, lw = ctx.w
+        spec = ctx.spec
+        dz, _, pg, pb, _ = K.ln_bwd(gout.contiguous(), z, m, r, lw)
+        df = K.dropout(dz, spec.p_drop, spec.seed) if spec.p_drop > 0 else dz
+        dwf = K.linear_wgrad(df, g)
+        dbf = _reduce(K.rows_colsum(df))
+        dpre = K.linear_dgrad(df, wf, out_dtype=torch.float32, epilogue=K.EPI_DGELU, aux=pre, resid=dz)
+        dwp = K.linear_wgrad(dpre, x)
+        dbp = _reduce(K.rows_colsum(dpre))
+        dx = K.linear_dgrad(dpre, wp, out_dtype=torch.float32)
+        return dx, None, dwp, dbp, dwf, dbf, _reduce(pg), _reduce(pb)
+
+
+# ------------------------------------------------------------- CLIP loss
+class ClipLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, I, T, temperature):
+        I = I.contiguous()
+        T = T.contiguous()
+        need = torch.is_grad_enabled() and (I.requires_grad or T.requires_grad)
+        loss, dI, dT = K.clip_loss(I, T, temperature, want_grad=True)
+        ctx.grads = (dI, dT)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        dI, dT = ctx.grads
+        ctx.grads = None
+        return dI * gl, dT * gl, None

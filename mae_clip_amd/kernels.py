@@ -1,0 +1,354 @@
+"""Thin torch-tensor wrappers over the libmaeclip C-ABI (include/maeclip.h).
+
+Every function launches on torch's current HIP stream, validates shapes on the
+host and raises MaeClipNativeError on any failure. Nothing here computes on the
+CPU: tensors must live on a ROCm device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+
+KC, RC = 0, 1
+EPI_NONE, EPI_GELU, EPI_RESID, EPI_DGELU = 0, 1, 2, 3
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return L.BF16
+    if t.dtype == torch.float32:
+        return L.F32
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.MaeClipNativeError("mae_clip_amd kernels need ROCm device tensors (no CPU fallback)")
+
+
+def _call(name, *args):
+    lib = L.lib()
+    rc = getattr(lib, name)(*args)
+    L.check(rc, name)
+
+
+# ------------------------------------------------------------------ GEMM
+def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=EPI_NONE, alpha=1.0, beta=0.0,
+         bias=None, aux=None, aux_out=None, ldaux=0, resid=None, ldr=0, colsum=None, batch=1,
+         strides=(0, 0, 0)):
+    _dev(A, B, Cout, bias, aux, aux_out, resid, colsum)
+    if A.dtype != B.dtype:
+        raise TypeError("gemm: A and B dtypes differ")
+    a = L.GemmArgs(A=A.data_ptr(), B=B.data_ptr(), C=Cout.data_ptr(), M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc,
+                   batch=batch, strideA=strides[0], strideB=strides[1], strideC=strides[2],
+                   dtype=_dt(A), out_dtype=_dt(Cout), a_layout=a_layout, b_layout=b_layout, epilogue=epilogue,
+                   alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
+                   resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum))
+    _call("maeclip_gemm", C.byref(a), _stream())
+
+
+def gemm_colsum_rows(M: int) -> int:
+    return int(L.lib().maeclip_gemm_colsum_rows(M))
+
+
+def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, aux_out=None, colsum=None):
+    """y[M,N] = x[M,K] w[N,K]^T (+bias) with epilogue (nn.Linear forward)."""
+    M, K = x.shape
+    N = w.shape[0]
+    out_dtype = out_dtype or x.dtype
+    y = torch.empty((M, N), device=x.device, dtype=out_dtype)
+    gemm(x, w, y, M, N, K, x.stride(0), w.stride(0), N, KC, KC, epilogue=epilogue, bias=bias, resid=resid,
+         ldr=(resid.stride(0) if resid is not None else 0), aux_out=aux_out,
+         ldaux=(aux_out.stride(0) if aux_out is not None else 0), colsum=colsum)
+    return y
+
+
+def linear_dgrad(dy, w, out_dtype=None, epilogue=EPI_NONE, aux=None, resid=None, colsum=None, out=None):
+    """dx[M,K] = dy[M,N] w[N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    out = out if out is not None else torch.empty((M, K), device=dy.device, dtype=out_dtype or dy.dtype)
+    gemm(dy, w, out, M, K, N, dy.stride(0), w.stride(0), out.stride(0), KC, RC, epilogue=epilogue, aux=aux,
+         ldaux=(aux.stride(0) if aux is not None else 0), resid=resid,
+         ldr=(resid.stride(0) if resid is not None else 0), colsum=colsum)
+    return out
+
+
+def linear_wgrad(dy, x, out=None, beta=0.0):
+    """dW[N,K] = dy[M,N]^T x[M,K]  (fp32)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    out = out if out is not None else torch.empty((N, K), device=dy.device, dtype=torch.float32)
+    gemm(dy, x, out, N, K, M, dy.stride(0), x.stride(0), out.stride(0), RC, RC, beta=beta)
+    return out
+
+
+# ------------------------------------------------------------- reductions
+def colsum_reduce(partial, out=None, accumulate=False, scale=1.0):
+    _dev(partial)
+    P, N = partial.shape
+    out = out if out is not None else torch.empty((N,), device=partial.device, dtype=torch.float32)
+    _call("maeclip_colsum_reduce", partial.data_ptr(), P, N, out.data_ptr(), int(accumulate), scale, _stream())
+    return out
+
+
+def rows_colsum(x, out_bf16=None):
+    """partial column sums [G, D] of x [M, D] (f32/bf16); optional bf16 copy."""
+    _dev(x, out_bf16)
+    M, D = x.shape
+    G = int(L.lib().maeclip_rows_colsum_partial_rows(M))
+    part = torch.empty((G, D), device=x.device, dtype=torch.float32)
+    _call("maeclip_rows_colsum", x.data_ptr(), _dt(x), M, D, x.stride(0), _ptr(out_bf16), part.data_ptr(), _stream())
+    return part
+
+
+def pool_fwd(x):
+    B, n, D = x.shape
+    out = torch.empty((B, D), device=x.device, dtype=torch.float32)
+    _call("maeclip_pool_fwd", x.data_ptr(), B, n, D, out.data_ptr(), _stream())
+    return out
+
+
+def pool_bwd(dout, n, dx=None, accumulate=False):
+    B, D = dout.shape
+    dx = dx if dx is not None else torch.empty((B, n, D), device=dout.device, dtype=torch.float32)
+    _call("maeclip_pool_bwd", dout.data_ptr(), B, n, D, dx.data_ptr(), int(accumulate), _stream())
+    return dx
+
+
+def dropout(x, p, seed, out=None):
+    M, D = x.shape
+    out = out if out is not None else torch.empty_like(x)
+    _call("maeclip_dropout", x.data_ptr(), out.data_ptr(), M, D, x.stride(0), float(p), int(seed), _stream())
+    return out
+
+
+def embed_fwd(ids, word, pos):
+    _dev(ids, word, pos)
+    B, T = ids.shape
+    V, D = word.shape
+    out = torch.empty((B * T, D), device=word.device, dtype=torch.float32)
+    _call("maeclip_embed_fwd", ids.data_ptr(), word.data_ptr(), pos.data_ptr(), B, T, D, V, out.data_ptr(), _stream())
+    return out
+
+
+# -------------------------------------------------------------- LayerNorm
+def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dropout=0.0, seed_in=0, seed_out=0,
+           want_stats=True, y2=False, xsum=False):
+    """Returns (y, mean, rstd, y2_bf16, xsum)."""
+    _dev(x, gamma, beta, res)
+    M, D = x.shape
+    dev = x.device
+    y = torch.empty((M, D), device=dev, dtype=out_dtype or x.dtype)
+    mean = torch.empty((M,), device=dev, dtype=torch.float32) if want_stats else None
+    rstd = torch.empty((M,), device=dev, dtype=torch.float32) if want_stats else None
+    yb = torch.empty((M, D), device=dev, dtype=torch.bfloat16) if y2 else None
+    xs = torch.empty((M, D), device=dev, dtype=torch.float32) if xsum else None
+    a = L.LnFwdArgs(x=x.data_ptr(), x_dtype=_dt(x), res=_ptr(res), ldres=(res.stride(0) if res is not None else 0),
+                    in_dropout_p=in_dropout, gamma=gamma.data_ptr(), beta=beta.data_ptr(), y=y.data_ptr(),
+                    y_dtype=_dt(y), y2=_ptr(yb), ldy2=D, xsum_out=_ptr(xs), ldxs=D, mean=_ptr(mean), rstd=_ptr(rstd),
+                    out_dropout_p=out_dropout, seed_in=int(seed_in), seed_out=int(seed_out),
+                    M=M, D=D, ldx=x.stride(0), ldy=D, eps=eps)
+    _call("maeclip_ln_fwd", C.byref(a), _stream())
+    return y, mean, rstd, yb, xs
+
+
+def ln_bwd_partial_rows(M: int) -> int:
+    return int(L.lib().maeclip_ln_bwd_partial_rows(M))
+
+
+def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False):
+    """Returns (dx f32, dx_bf16, dgamma_partial, dbeta_partial, dx_colsum_partial)."""
+    _dev(dy, x, mean, rstd, gamma, dres)
+    M, D = x.shape
+    dev = x.device
+    G = ln_bwd_partial_rows(M)
+    dx = torch.empty((M, D), device=dev, dtype=torch.float32)
+    dxb = torch.empty((M, D), device=dev, dtype=torch.bfloat16) if want_bf16 else None
+    pg = torch.empty((G, D), device=dev, dtype=torch.float32) if want_param_grads else None
+    pb = torch.empty((G, D), device=dev, dtype=torch.float32) if want_param_grads else None
+    pc = torch.empty((G, D), device=dev, dtype=torch.float32) if want_colsum else None
+    a = L.LnBwdArgs(dy=dy.data_ptr(), dy_dtype=_dt(dy), x=x.data_ptr(), x_dtype=_dt(x), mean=mean.data_ptr(),
+                    rstd=rstd.data_ptr(), gamma=gamma.data_ptr(), dres=_ptr(dres), dx=dx.data_ptr(), dx_bf=_ptr(dxb),
+                    lddx_bf=D, dgamma_partial=_ptr(pg), dbeta_partial=_ptr(pb), dx_colsum_partial=_ptr(pc),
+                    M=M, D=D, ldx=x.stride(0), lddy=dy.stride(0), lddx=D)
+    _call("maeclip_ln_bwd", C.byref(a), _stream())
+    return dx, dxb, pg, pb, pc
+
+
+# -------------------------------------------------------------- attention
+def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True):
+    _dev(qkv, key_mask)
+    D = H * hd
+    o = torch.empty((B * n, D), device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty((B, H, n), device=qkv.device, dtype=torch.float32) if want_lse else None
+    a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=_ptr(lse), dout=None, dqkv=None, key_mask=_ptr(key_mask),
+                   colsum_partial=None, ld_qkv=qkv.stride(0), ld_o=D, ld_dqkv=0, B=B, n=n, H=H, head_dim=hd,
+                   dtype=_dt(qkv), scale=scale, dropout_p=dropout_p, seed=int(seed))
+    _call("maeclip_attn_fwd", C.byref(a), _stream())
+    return o, lse
+
+
+def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True):
+    _dev(qkv, o, dout, lse)
+    D = H * hd
+    dqkv = torch.empty((B * n, 3 * D), device=qkv.device, dtype=qkv.dtype)
+    part = torch.empty((B, 3 * D), device=qkv.device, dtype=torch.float32) if want_colsum else None
+    a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(), dout=dout.data_ptr(), dqkv=dqkv.data_ptr(),
+                   key_mask=None, colsum_partial=_ptr(part), ld_qkv=qkv.stride(0), ld_o=o.stride(0),
+                   ld_dqkv=3 * D, B=B, n=n, H=H, head_dim=hd, dtype=_dt(qkv), scale=scale, dropout_p=0.0, seed=0)
+    _call("maeclip_attn_bwd", C.byref(a), _stream())
+    return dqkv, part
+
+
+# --------------------------------------------------------------------- MAE
+def mask_ids(B, L_, len_keep, seed, step, sample_offset, device, want_noise=False):
+    ids_shuffle = torch.empty((B, L_), device=device, dtype=torch.int32)
+    ids_restore = torch.empty((B, L_), device=device, dtype=torch.int32)
+    mask = torch.empty((B, L_), device=device, dtype=torch.float32)
+    noise = torch.empty((B, L_), device=device, dtype=torch.float32) if want_noise else None
+    a = L.MaskArgs(ids_shuffle=ids_shuffle.data_ptr(), ids_restore=ids_restore.data_ptr(), mask=mask.data_ptr(),
+                   noise=_ptr(noise), B=B, L=L_, len_keep=len_keep, seed=int(seed), step=int(step),
+                   sample_offset=int(sample_offset))
+    _call("maeclip_mask_ids", C.byref(a), _stream())
+    return ids_shuffle, ids_restore, mask, noise
+
+
+def patch_gather(img, ids_shuffle, keep, p, kpad, dtype):
+    _dev(img, ids_shuffle)
+    B, Cc, S, _ = img.shape
+    out = torch.empty((B * keep, kpad), device=img.device, dtype=dtype)
+    a = L.PatchArgs(img=img.data_ptr(), ids_shuffle=_ptr(ids_shuffle), out=out.data_ptr(), ld_out=kpad, B=B, C=Cc, S=S,
+                    p=p, keep=keep, dtype=_dt(out))
+    _call("maeclip_patch_gather", C.byref(a), _stream())
+    return out
+
+
+def tokens_fwd(y, ids_shuffle, pos, cls, B, L_, keep):
+    D = pos.shape[-1]
+    x = torch.empty((B, keep + 1, D), device=y.device, dtype=torch.float32)
+    a = L.TokensArgs(y=y.data_ptr(), ldy=y.stride(0), ids_shuffle=_ptr(ids_shuffle), ids_restore=None,
+                     pos=pos.data_ptr(), cls=cls.data_ptr(), x=x.data_ptr(), dx=None, dy=None, dpos=None, dcls=None,
+                     B=B, L=L_, keep=keep, D=D, dtype=_dt(y))
+    _call("maeclip_tokens_fwd", C.byref(a), _stream())
+    return x
+
+
+def tokens_bwd(dx, ids_restore, B, L_, keep, dy_dtype):
+    D = dx.shape[-1]
+    dy = torch.empty((B * keep, D), device=dx.device, dtype=dy_dtype)
+    dpos = torch.empty((L_ + 1, D), device=dx.device, dtype=torch.float32)
+    dcls = torch.empty((D,), device=dx.device, dtype=torch.float32)
+    a = L.TokensArgs(y=None, ldy=D, ids_shuffle=None, ids_restore=_ptr(ids_restore), pos=None, cls=None, x=None,
+                     dx=dx.data_ptr(), dy=dy.data_ptr(), dpos=dpos.data_ptr(), dcls=dcls.data_ptr(),
+                     B=B, L=L_, keep=keep, D=D, dtype=_dt(dy))
+    _call("maeclip_tokens_bwd", C.byref(a), _stream())
+    return dy, dpos, dcls
+
+
+def unshuffle_fwd(y, ids_restore, mask_token, pos, B, L_, keep):
+    D = pos.shape[-1]
+    out = torch.empty((B, L_ + 1, D), device=y.device, dtype=torch.float32)
+    a = L.UnshuffleArgs(y=y.data_ptr(), ldy=y.stride(0), ids_shuffle=None, ids_restore=ids_restore.data_ptr(),
+                        mask_token=mask_token.data_ptr(), pos=pos.data_ptr(), out=out.data_ptr(), dout=None, dy=None,
+                        dmask_partial=None, colsum_partial=None, B=B, L=L_, keep=keep, D=D, dtype=L.F32)
+    _call("maeclip_unshuffle_fwd", C.byref(a), _stream())
+    return out
+
+
+def unshuffle_bwd(dout, ids_shuffle, B, L_, keep, dy_dtype):
+    D = dout.shape[-1]
+    dy = torch.empty((B * (keep + 1), D), device=dout.device, dtype=dy_dtype)
+    dmask = torch.empty((B, D), device=dout.device, dtype=torch.float32)
+    cs = torch.empty((B, D), device=dout.device, dtype=torch.float32)
+    a = L.UnshuffleArgs(y=None, ldy=D, ids_shuffle=ids_shuffle.data_ptr(), ids_restore=None, mask_token=None, pos=None,
+                        out=None, dout=dout.data_ptr(), dy=dy.data_ptr(), dmask_partial=dmask.data_ptr(),
+                        colsum_partial=cs.data_ptr(), B=B, L=L_, keep=keep, D=D, dtype=_dt(dy))
+    _call("maeclip_unshuffle_bwd", C.byref(a), _stream())
+    return dy, dmask, cs
+
+
+def mae_loss_fwd(pred, img, mask, p, norm_pix):
+    B, Cc, S, _ = img.shape
+    L_ = mask.shape[1]
+    row = torch.empty((B * L_,), device=img.device, dtype=torch.float32)
+    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
+                      row_loss=row.data_ptr(), dpred=None, lddp=0, grad_out=None, colsum_partial=None,
+                      loss_scale=1.0, mask_count=1.0, B=B, C=Cc, S=S, p=p, L=L_, norm_pix=int(norm_pix),
+                      dtype=_dt(pred))
+    _call("maeclip_mae_loss_fwd", C.byref(a), _stream())
+    return row
+
+
+def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=1.0):
+    B, Cc, S, _ = img.shape
+    L_ = mask.shape[1]
+    P = Cc * p * p
+    dpred = torch.empty_like(pred)
+    cs = torch.empty((B, P), device=img.device, dtype=torch.float32)
+    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
+                      row_loss=None, dpred=dpred.data_ptr(), lddp=dpred.stride(0), grad_out=_ptr(grad_out),
+                      colsum_partial=cs.data_ptr(), loss_scale=loss_scale, mask_count=float(mask_count),
+                      B=B, C=Cc, S=S, p=p, L=L_, norm_pix=int(norm_pix), dtype=_dt(pred))
+    _call("maeclip_mae_loss_bwd", C.byref(a), _stream())
+    return dpred, cs
+
+
+# --------------------------------------------------------------- CLIP loss
+def clip_loss(I, T, temperature, want_grad=True):
+    _dev(I, T)
+    N, P = I.shape
+    ws_bytes = int(L.lib().maeclip_clip_loss_workspace(N))
+    ws = torch.empty((ws_bytes // 4,), device=I.device, dtype=torch.float32)
+    loss = torch.empty((), device=I.device, dtype=torch.float32)
+    dI = torch.empty_like(I) if want_grad else None
+    dT = torch.empty_like(T) if want_grad else None
+    a = L.ClipArgs(I=I.data_ptr(), T=T.data_ptr(), ld_I=I.stride(0), ld_T=T.stride(0), N=N, P=P,
+                   temperature=float(temperature), loss=loss.data_ptr(), row_loss_out=None, dI=_ptr(dI), dT=_ptr(dT),
+                   ld_dI=P, ld_dT=P, workspace=ws.data_ptr(), ws_bytes=ws_bytes)
+    _call("maeclip_clip_loss", C.byref(a), _stream())
+    return loss, dI, dT
+
+
+# ------------------------------------------------------------ multi-tensor
+class MultiTensorPlan:
+    """Host + device entry arrays for one multi-tensor launch."""
+
+    def __init__(self, entries, device):
+        chunk = int(L.lib().maeclip_mt_chunk())
+        n = len(entries)
+        self.host = (L.MtEntry * n)()
+        start = 0
+        for i, e in enumerate(entries):
+            h = self.host[i]
+            h.p0, h.p1, h.p2, h.p3, h.p4 = e[:5]
+            h.n = e[5]
+            h.chunk_start = start
+            start += (e[5] + chunk - 1) // chunk
+        raw = bytes(self.host)
+        self.dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.n = n
+
+
+def cast_multi(plan: MultiTensorPlan):
+    _call("maeclip_cast_multi", plan.dev.data_ptr(), plan.host, plan.n, _stream())
+
+
+def adamw_multi(plan: MultiTensorPlan, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    hp = L.AdamwHparams(lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay, step_size=lr / bc1,
+                        bc2_sqrt=bc2 ** 0.5, grad_scale=grad_scale)
+    _call("maeclip_adamw_multi", plan.dev.data_ptr(), plan.host, plan.n, C.byref(hp), _stream())

@@ -1,0 +1,174 @@
+"""Kernel-level numerics: each HIP kernel vs a plain PyTorch fp32/fp64 reference
+of the same op (same seeded inputs). Runs on the GPU box only."""
+import math
+
+import pytest
+import torch
+
+from mae_clip_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, dtype, dev, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(dtype).to(dev)
+
+
+def _ref_mm(A, B):
+    return (A.double() @ B.double())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("lay", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mnk", [(256, 256, 128), (200, 136, 72), (16, 8, 64), (384, 640, 1024)])
+def test_gemm_layouts(dev, dtype, lay, mnk):
+    M, N, Kd = mnk
+    a_lay, b_lay = lay
+    A = _rand((M, Kd) if a_lay == 0 else (Kd, M), dtype, dev, seed=1)
+    B = _rand((N, Kd) if b_lay == 0 else (Kd, N), dtype, dev, seed=2)
+    C = torch.empty((M, N), device=dev, dtype=torch.float32)
+    K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, a_lay, b_lay, alpha=0.5)
+    Am = A if a_lay == 0 else A.t()
+    Bm = B.t() if b_lay == 0 else B
+    ref = 0.5 * _ref_mm(Am, Bm)
+    err = (C.double() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err / scale < (2e-6 if dtype == torch.float32 else 2e-5) * math.sqrt(Kd), (err, scale)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dev, dtype):
+    M, N, Kd = 300, 384, 256
+    x = _rand((M, Kd), dtype, dev, seed=3)
+    w = _rand((N, Kd), dtype, dev, scale=0.05, seed=4)
+    bias = _rand((N,), torch.float32, dev, seed=5)
+    resid = _rand((M, N), torch.float32, dev, seed=6)
+    ref = _ref_mm(x, w.t()) + bias.double()
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    # bias + gelu (pre stored to aux_out)
+    pre = torch.empty((M, N), device=dev, dtype=dtype)
+    y = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU, aux_out=pre)
+    assert (pre.double() - ref).abs().max().item() < tol * 4
+    assert (y.double() - torch.nn.functional.gelu(ref)).abs().max().item() < tol * 4
+    # residual
+    y2 = K.linear_fwd(x, w, bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=resid)
+    assert (y2.double() - (ref + resid.double())).abs().max().item() < tol * 4
+    # colsum partial
+    part = torch.empty((K.gemm_colsum_rows(M), N), device=dev, dtype=torch.float32)
+    y3 = K.linear_fwd(x, w, bias, out_dtype=torch.float32, colsum=part)
+    cs = K.colsum_reduce(part)
+    assert (cs.double() - y3.double().sum(0)).abs().max().item() < 1e-3
+    # dgelu: dx = (dy @ w) * gelu'(aux)
+    dy = _rand((M, N), dtype, dev, seed=7)
+    aux = _rand((M, Kd), dtype, dev, seed=8)
+    dx = K.linear_dgrad(dy, w, epilogue=K.EPI_DGELU, aux=aux, out_dtype=torch.float32)
+    a64 = aux.double().requires_grad_(True)
+    g = torch.autograd.grad(torch.nn.functional.gelu(a64).sum(), a64)[0]
+    ref_dx = _ref_mm(dy, w) * g
+    assert (dx.double() - ref_dx).abs().max().item() < tol * 4
+    # wgrad
+    dW = K.linear_wgrad(dy, x)
+    assert (dW.double() - _ref_mm(dy.t(), x)).abs().max().item() / _ref_mm(dy.t(), x).abs().max().item() < 1e-4
+
+
+def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
+    q, k, v = qkv.double().view(B, n, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    if key_mask is not None:
+        s = s.masked_fill(key_mask.view(B, 1, 1, n) == 0, float("-inf"))
+    p = s.softmax(-1)
+    return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64)])
+def test_attention_fwd_bwd(dev, dtype, shape):
+    B, n, H, hd = shape
+    if dtype == torch.float32 and n > 100:
+        pytest.skip("fp32 image of this length exceeds LDS (parity runs use short sequences)")
+    scale = hd ** -0.5
+    qkv = _rand((B * n, 3 * H * hd), dtype, dev, seed=11)
+    o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
+    ref = _attn_ref(qkv, B, n, H, hd, scale)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert (o.double() - ref).abs().max().item() < tol
+    # backward vs autograd fp64
+    dout = _rand((B * n, H * hd), dtype, dev, seed=12)
+    dqkv, part = K.attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale)
+    x64 = qkv.double().detach().requires_grad_(True)
+    r = _attn_ref(x64, B, n, H, hd, scale)
+    (r * dout.double()).sum().backward()
+    g = x64.grad
+    gs = g.abs().max().item()
+    tolb = 1e-4 if dtype == torch.float32 else 3e-2
+    assert (dqkv.double() - g).abs().max().item() / gs < tolb
+    cs = part.sum(0)
+    assert (cs.double() - g.view(B, n, -1).sum(1).sum(0)).abs().max().item() / (gs * n) < tolb
+
+
+def test_attention_key_mask(dev):
+    B, n, H, hd = 3, 25, 4, 64
+    qkv = _rand((B * n, 3 * H * hd), torch.bfloat16, dev, seed=13)
+    km = torch.ones((B, n), device=dev)
+    km[1, 10:] = 0
+    km[2, 3:] = 0
+    o, _ = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
+    ref = _attn_ref(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
+    assert (o.double() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(dev, dtype):
+    M, D = 333, 768
+    x = _rand((M, D), torch.float32, dev, seed=21) * 3 + 1
+    res = _rand((M, D), torch.float32, dev, seed=22)
+    g = _rand((D,), torch.float32, dev, seed=23)
+    b = _rand((D,), torch.float32, dev, seed=24)
+    y, mean, rstd, yb, xs = K.ln_fwd(x, g, b, 1e-6, out_dtype=dtype, res=res, y2=True, xsum=True)
+    xr = (x + res).double()
+    ref = torch.nn.functional.layer_norm(xr, (D,), g.double(), b.double(), 1e-6)
+    rel = 1e-6 if dtype == torch.float32 else 2 ** -8  # bf16 output rounding
+    assert ((y.double() - ref).abs() - rel * ref.abs()).max().item() < 1e-4
+    assert (xs.double() - xr).abs().max().item() < 1e-5
+    dy = _rand((M, D), torch.float32, dev, seed=25)
+    dres = _rand((M, D), torch.float32, dev, seed=26)
+    dx, dxb, pg, pb, pc = K.ln_bwd(dy, xs, mean, rstd, g, dres=dres, want_bf16=True, want_colsum=True)
+    x64 = xr.clone().requires_grad_(True)
+    g64 = g.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True)
+    out = torch.nn.functional.layer_norm(x64, (D,), g64, b64, 1e-6)
+    (out * dy.double()).sum().backward()
+    assert (dx.double() - (x64.grad + dres.double())).abs().max().item() < 1e-3
+    assert (K.colsum_reduce(pg).double() - g64.grad).abs().max().item() < 1e-2
+    assert (K.colsum_reduce(pb).double() - b64.grad).abs().max().item() < 1e-2
+    assert (K.colsum_reduce(pc).double() - dx.double().sum(0)).abs().max().item() < 1e-2
+
+
+def test_clip_loss_kernel_vs_torch(dev):
+    for N in (8, 64, 256):
+        I = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=31), (256,))
+        T = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=32), (256,))
+        loss, dI, dT = K.clip_loss(I, T, 1.0)
+        I64 = I.double().requires_grad_(True)
+        T64 = T.double().requires_grad_(True)
+        logits = T64 @ I64.T
+        tgt = torch.softmax((I64 @ I64.T + T64 @ T64.T) / 2, -1)
+        lt = (-tgt * torch.log_softmax(logits, -1)).sum(1)
+        li = (-tgt.T * torch.log_softmax(logits.T, -1)).sum(1)
+        ref = ((li + lt) / 2).mean()
+        ref.backward()
+        assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+        assert (dI.double() - I64.grad).abs().max().item() < 1e-5
+        assert (dT.double() - T64.grad).abs().max().item() < 1e-5
+
+
+def test_mask_ids_is_stable_argsort(dev):
+    B, L_, keep = 16, 196, 49
+    ids_s, ids_r, mask, noise = K.mask_ids(B, L_, keep, seed=2, step=5, sample_offset=0, device=dev, want_noise=True)
+    ref_s = torch.argsort(noise.cpu(), dim=1, stable=True)
+    assert torch.equal(ids_s.cpu().long(), ref_s)
+    assert torch.equal(ids_r.cpu().long(), torch.argsort(ref_s, dim=1))
+    m = torch.ones(B, L_)
+    m[:, :keep] = 0
+    assert torch.equal(mask.cpu(), torch.gather(m, 1, ids_r.cpu().long()))
