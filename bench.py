@@ -1,0 +1,236 @@
+"""Headline benchmark: images/sec of one ViT-B/16 CLIP+MAE training step
+(BASELINE.json metric).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Workload per GPU = BASELINE.json configs[2] / configs[3]: ViT-B/16 @224, 256
+images per GPU, MAE mask 0.75 + 8-layer 512-d decoder, 6-layer frozen
+DistilBERT text tower (T=25), soft-target CLIP loss over the GLOBAL batch
+(embeddings all-gathered), fused AdamW -- forward + backward + optimizer every
+step, bf16 MFMA with fp32 master weights. Synthetic inputs already resident in
+HBM (uint8 pixels ImageNet-normalised, input_ids randint(5,300)).
+Weak scaling: per-GPU batch fixed, value = global images / max-over-ranks time.
+
+Extra fields: "roofline" (dominant kernel, timed live with HIP events on its
+stream during the timed steps), "cpu_baseline" (the CPU oracle of /oracle on a
+bounded sample, rank 0 at N=1 only), "loss_delta_vs_ref" (C0 fp32 parity).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+IMG_FLOPS_C2 = 60.2e9       # algorithmic FLOP / image, SURVEY.md §8d / Appendix C
+
+
+def synthetic_batch(B, S, T, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    px = torch.randint(0, 256, (B, 3, S, S), generator=g, dtype=torch.uint8).to(device)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1)
+    img = ((px.float() / 255.0) - mean) / std
+    ids = torch.randint(5, 300, (B, T), generator=g).to(device)
+    am = torch.ones(B, T, dtype=torch.int64, device=device)
+    return {"image": img.contiguous(), "input_ids": ids, "attention_mask": am}
+
+
+def build_model(cfg_over):
+    from mae_clip_amd import config as CFG
+    for k, v in cfg_over.items():
+        setattr(CFG, k, v)
+    from mae_clip_amd.CLIP import CLIPModel
+    return CLIPModel()
+
+
+def parity_c0(device):
+    """|loss(product, fp32 parity mode) - loss(CPU oracle, fp64)| at C0 (ViT-Tiny @32,
+    2-layer text, mask .75, B=8) -- the 'loss delta vs ref' of the metric."""
+    sys.path.insert(0, ROOT)
+    from tests.helpers import build_pair, make_batch
+    prod, ref = build_pair("fp32")
+    prod.eval()
+    ref.eval()
+    b = make_batch(8, 32)
+    with torch.no_grad():
+        lp = prod({k: v.to(device) for k, v in b.items()}).item()
+        lr = ref(dict(b, image=b["image"].double())).item()
+    return abs(lp - lr), lp, lr
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """The CPU oracle (pure torch fp32, same ops as the reference) on a bounded
+    sample of the same workload: ViT-B/16 MAE+CLIP, 6-layer text, B=16."""
+    from oracle.ref_model import CLIPModel as RefCLIP, OracleConfig
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    torch.set_num_threads(threads)
+    cfg = OracleConfig(model_name="vit_base_patch16_224", img_size=224, text_layers=6, mask_ratio=0.75,
+                       decoder_dim=512, decoder_depth=8, decoder_heads=16)
+    torch.manual_seed(0)
+    m = RefCLIP(cfg)
+    m.train()
+    opt = torch.optim.AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    B = 16
+    batch = synthetic_batch(B, 224, 25, 0, "cpu")
+    times = []
+    t_start = time.perf_counter()
+    for i in range(4):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        loss = m(batch)
+        loss.backward()
+        opt.step()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > seconds_budget and i >= 1:
+            break
+    timed = times[1:] if len(times) > 1 else times
+    per_step = sorted(timed)[len(timed) // 2]
+    return {"value": B / per_step, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle ViT-B/16 MAE+CLIP + 6-layer text, fp32 CPU, B={B}, median of {len(timed)} "
+                      f"step(s) after 1 warm-up (fwd+bwd+AdamW)"}
+
+
+class KernelTimer:
+    """Brackets every GEMM launch with HIP events on the launching stream during
+    the timed steps; reports the (shape) with the largest total time."""
+
+    def __init__(self):
+        self.records = {}
+        self.active = False
+
+    def hook(self, key, flops, launch):
+        if not self.active:
+            return launch()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        self.records.setdefault(key, [flops, []])[1].append((s, e))
+
+    def summary(self):
+        best = None
+        for key, (flops, evs) in self.records.items():
+            ms = [a.elapsed_time(b) for a, b in evs]
+            tot = sum(ms)
+            if best is None or tot > best[2]:
+                best = (key, flops, tot, len(ms))
+        return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--mask-ratio", type=float, default=0.75)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from mae_clip_amd import kernels as K
+    from mae_clip_amd.optim import AdamW
+    from mae_clip_amd.distributed import DataParallel
+
+    model = build_model(dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6,
+                             mask_ratio=args.mask_ratio, decoder_embed_dim=512, decoder_depth=8,
+                             decoder_num_heads=16, precision="bf16")).to(device)
+    model.train()
+    dp = DataParallel(model) if world > 1 else None
+    opt = AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    batch = synthetic_batch(args.batch, 224, 25, 1000 + rank, device)
+
+    timer = KernelTimer()
+    if not args.no_kernel_timer:
+        K.LAUNCH_HOOK = timer.hook
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = model(batch)
+        loss.backward()
+        if dp is not None:
+            dp.sync_gradients()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+        loss.item()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer.active = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+        loss.item()  # main.py:64 syncs every step
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.active = False
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    global_batch = args.batch * world
+    value = global_batch * args.steps / elapsed
+    ms = elapsed / args.steps * 1000.0
+
+    if rank == 0:
+        roof = None
+        best = timer.summary() if not args.no_kernel_timer else None
+        if best is not None:
+            key, flops, tot_ms, nl = best
+            avg_s = tot_ms / nl / 1000.0
+            ach = flops / avg_s / 1e12
+            roof = {"bound": "mfma", "kernel": "gemm " + key, "achieved": round(ach, 1),
+                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                    "traffic": None, "avg_launch_us": round(avg_s * 1e6, 1), "launches": nl,
+                    "step_tflops": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12, 1),
+                    "step_frac": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12 / PEAK_BF16_TFLOPS, 4)}
+        out = {"metric": "images/sec/node ViT-B/16 CLIP+MAE step", "value": round(value, 2), "unit": "images/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (uint8 pixels ImageNet-normalised, input_ids randint(5,300)), random-init weights",
+               "config": {"workload": "C2/C3: ViT-B/16 224 MAE(0.75)+CLIP, 8x512 decoder, DistilBERT-6 frozen "
+                                      "T=25, AdamW, bf16 MFMA / fp32 master",
+                          "global_batch": global_batch, "per_gpu_batch": args.batch, "image_size": 224,
+                          "mask_ratio": args.mask_ratio, "parallelism": f"dp{world}"},
+               "loss": round(loss.item(), 4), "roofline": roof}
+        if world == 1 and not args.no_parity:
+            try:
+                dl, lp, lr = parity_c0(device)
+                out["loss_delta_vs_ref"] = {"abs": dl, "product": lp, "oracle": lr,
+                                            "config": "C0 ViT-Tiny/16@32, 2-layer text, mask .75, B=8, fp32"}
+            except Exception as e:  # reported, never hides the perf line
+                out["loss_delta_vs_ref"] = {"error": repr(e)}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

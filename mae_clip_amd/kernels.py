@@ -15,6 +15,10 @@ from . import _lib as L
 KC, RC = 0, 1
 EPI_NONE, EPI_GELU, EPI_RESID, EPI_DGELU = 0, 1, 2, 3
 
+# Optional instrumentation: LAUNCH_HOOK(key, flops, launch_fn) wraps every GEMM
+# launch (bench.py brackets them with HIP events on the current stream).
+LAUNCH_HOOK = None
+
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
@@ -56,7 +60,12 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
                    dtype=_dt(A), out_dtype=_dt(Cout), a_layout=a_layout, b_layout=b_layout, epilogue=epilogue,
                    alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
                    resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum))
-    _call("maeclip_gemm", C.byref(a), _stream())
+    if LAUNCH_HOOK is None:
+        _call("maeclip_gemm", C.byref(a), _stream())
+    else:
+        key = (f"M{M} N{N} K{K} {'KR'[a_layout]}{'KR'[b_layout]} epi{epilogue} "
+               f"{'bf16' if A.dtype == torch.bfloat16 else 'f32'}")
+        LAUNCH_HOOK(key, 2.0 * M * N * K * batch, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
 
 
 def gemm_colsum_rows(M: int) -> int:
