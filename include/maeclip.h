@@ -49,7 +49,11 @@ int32_t maeclip_device_count(void);
  *           2 residual (C(f32) <- resid + acc (+bias)); 3 dGELU (C <- acc *
  *           gelu'(aux) (+ resid if resid != NULL)).
  * colsum_partial (optional, f32 [batch*maeclip_gemm_colsum_rows(M)][N]):
- *   per-block column sums of the final C, reduce with maeclip_colsum_reduce. */
+ *   per-block column sums of the final C, reduce with maeclip_colsum_reduce.
+ * splitk > 1 (epilogue 0, no colsum): K is cut into splitk slices whose fp32
+ *   partial tiles go to workspace [batch][splitk][M][N]; a second launch sums
+ *   them in fixed order (+bias, +beta*C) -> deterministic. Use
+ *   maeclip_gemm_splitk(M,N,K) for the slice count. */
 typedef struct {
   const void* A;
   const void* B;
@@ -69,9 +73,12 @@ typedef struct {
   const float* resid;
   int64_t ldr;
   float* colsum_partial;
+  int32_t splitk;
+  float* workspace;
 } maeclip_gemm_args;
 int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
 int64_t maeclip_gemm_colsum_rows(int64_t M);
+int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K);
 
 /* ------------------------------------------------------------- attention
  * Replaces F.scaled_dot_product_attention in timm Attention / HF ViTMAE
@@ -149,9 +156,10 @@ int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* args, void* stream);
 int32_t maeclip_ln_bwd_partial_rows(int64_t M);
 
 /* ------------------------------------------------------------ reductions */
-/* out[n] (+)= scale * sum_p partial[p*N + n]  (fixed order -> deterministic) */
+/* out[n] (+)= scale * sum_p partial[p*N + n]  (fixed order -> deterministic);
+ * two passes when P > 64 (scratch: f32 [ceil(P/64)][N], may be NULL otherwise) */
 int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate, float scale,
-                              void* stream);
+                              float* scratch, void* stream);
 /* partial column sums of a [M, D] row matrix (dtype f32/bf16, row stride ld)
  * into partial [maeclip_rows_colsum_partial_rows(M)][D]; optional bf16 copy
  * out_bf16 [M, D]. */

@@ -26,7 +26,8 @@ class GemmArgs(C.Structure):
                 ("dtype", c_i32), ("out_dtype", c_i32), ("a_layout", c_i32), ("b_layout", c_i32),
                 ("epilogue", c_i32), ("alpha", c_f32), ("beta", c_f32),
                 ("bias", c_vp), ("aux", c_vp), ("aux_out", c_vp), ("ldaux", c_i64),
-                ("resid", c_vp), ("ldr", c_i64), ("colsum_partial", c_vp)]
+                ("resid", c_vp), ("ldr", c_i64), ("colsum_partial", c_vp),
+                ("splitk", c_i32), ("workspace", c_vp)]
 
 
 class AttnArgs(C.Structure):
@@ -108,12 +109,13 @@ _SIGS = {
     "maeclip_device_count": (c_i32, []),
     "maeclip_gemm": (c_i32, [C.POINTER(GemmArgs), c_vp]),
     "maeclip_gemm_colsum_rows": (c_i64, [c_i64]),
+    "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
     "maeclip_attn_fwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_attn_bwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_ln_fwd": (c_i32, [C.POINTER(LnFwdArgs), c_vp]),
     "maeclip_ln_bwd": (c_i32, [C.POINTER(LnBwdArgs), c_vp]),
     "maeclip_ln_bwd_partial_rows": (c_i32, [c_i64]),
-    "maeclip_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_f32, c_vp]),
+    "maeclip_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_f32, c_vp, c_vp]),
     "maeclip_rows_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),

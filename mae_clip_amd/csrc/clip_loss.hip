@@ -158,7 +158,7 @@ extern "C" int32_t maeclip_clip_loss(const maeclip_clip_args* a, void* stream) {
   hipLaunchKernelGGL(grad_kernel, dim3((unsigned)N), dim3(NTH), 0, s, Lm, Y, lse_r, lse_c, cy, S, dL, rl, (int)N,
                      grad ? 1 : 0);
   MC_CHECK_LAUNCH("maeclip_clip_loss(stats)");
-  if ((e = maeclip_colsum_reduce(rl, N, 1, a->loss, 0, 1.f, s))) return e;
+  if ((e = maeclip_colsum_reduce(rl, N, 1, a->loss, 0, 1.f, nullptr, s))) return e;
   if (a->row_loss_out) (void)hipMemcpyAsync(a->row_loss_out, rl, N * sizeof(float), hipMemcpyDeviceToDevice, s);
   if (!grad) return 0;
   float* Dm = Y;

@@ -27,6 +27,26 @@ __global__ void __launch_bounds__(NTH) colsum_reduce_kernel(const float* __restr
   out[n] = accumulate ? out[n] + s : s;
 }
 
+// pass 1 of a tall reduction: block (64 columns x 64 rows) -> one row of scratch
+__global__ void __launch_bounds__(NTH) colsum_pass1_kernel(const float* __restrict__ part, int64_t P, int64_t N,
+                                                           float* __restrict__ scratch) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + c;
+  const int64_t r0 = (int64_t)blockIdx.y * 64;
+  float s = 0.f;
+  if (n < N) {
+#pragma unroll 4
+    for (int i = ph; i < 64; i += 4) {
+      const int64_t r = r0 + i;
+      if (r < P) s += part[r * N + n];
+    }
+  }
+  red[ph][c] = s;
+  __syncthreads();
+  if (ph == 0 && n < N) scratch[(int64_t)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
 // single-vector sum (P large, N == 1): one workgroup, fixed-order tree
 __global__ void __launch_bounds__(NTH) vec_sum_kernel(const float* __restrict__ x, int64_t P, float* __restrict__ out,
                                                       int accumulate, float scale) {
@@ -204,9 +224,17 @@ int64_t mt_blocks(const maeclip_mt_entry* host_entries, int ne) {
 extern "C" int64_t maeclip_mt_chunk(void) { return CHUNK; }
 
 extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate,
-                                         float scale, void* stream) {
+                                         float scale, float* scratch, void* stream) {
   MC_CHECK_ARG(partial && out && P >= 1 && N >= 1, "maeclip_colsum_reduce: bad args");
   hipStream_t s = (hipStream_t)stream;
+  if (N > 1 && P > 64) {
+    MC_CHECK_ARG(scratch != nullptr, "maeclip_colsum_reduce: P > 64 needs scratch [ceil(P/64)][N]");
+    dim3 g1((unsigned)((N + 63) / 64), (unsigned)((P + 63) / 64));
+    hipLaunchKernelGGL(colsum_pass1_kernel, g1, dim3(NTH), 0, s, partial, P, N, scratch);
+    MC_CHECK_LAUNCH("maeclip_colsum_reduce(pass1)");
+    partial = scratch;
+    P = (P + 63) / 64;
+  }
   if (N == 1) {
     hipLaunchKernelGGL(vec_sum_kernel, dim3(1), dim3(NTH), 0, s, partial, P, out, accumulate, scale);
   } else {

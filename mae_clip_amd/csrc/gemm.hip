@@ -192,9 +192,14 @@ gemm_kernel(const maeclip_gemm_args args) {
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   v4u ra[4], rb[4];
-  const int nt = (K + BK - 1) / BK;
-  stage_load<T, LA>(ra, A, args.lda, m0, M, 0, K, tid);
-  stage_load<T, LB>(rb, B, args.ldb, n0, N, 0, K, tid);
+  // split-K slice [kbeg, kend) (whole K when splitk == 1)
+  const int S = args.splitk > 1 ? args.splitk : 1;
+  const int klen = ((K + S - 1) / S + BK - 1) / BK * BK;
+  const int kbeg = blockIdx.y * klen;
+  const int kend = min(K, kbeg + klen);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  stage_load<T, LA>(ra, A, args.lda, m0, M, kbeg, kend, tid);
+  stage_load<T, LB>(rb, B, args.ldb, n0, N, kbeg, kend, tid);
   stage_store<T, LA>(LDS_A(0), ra, tid);
   stage_store<T, LB>(LDS_B(0), rb, tid);
   __syncthreads();
@@ -203,8 +208,8 @@ gemm_kernel(const maeclip_gemm_args args) {
     const int cur = t & 1;
     const bool more = (t + 1) < nt;
     if (more) {
-      stage_load<T, LA>(ra, A, args.lda, m0, M, (t + 1) * BK, K, tid);
-      stage_load<T, LB>(rb, B, args.ldb, n0, N, (t + 1) * BK, K, tid);
+      stage_load<T, LA>(ra, A, args.lda, m0, M, kbeg + (t + 1) * BK, kend, tid);
+      stage_load<T, LB>(rb, B, args.ldb, n0, N, kbeg + (t + 1) * BK, kend, tid);
     }
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
@@ -228,6 +233,19 @@ gemm_kernel(const maeclip_gemm_args args) {
 
   // ---------------- epilogue: lane owns C[m][n..n+3]
   const int g = lane >> 4;
+  if (S > 1) {  // split-K: raw fp32 partial tile -> workspace slab (reduced by splitk_reduce_kernel)
+    float* slab = args.workspace + ((int64_t)z * S + blockIdx.y) * (int64_t)M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + 16 * j + 4 * g;
+        if (m < M && n < N) *(v4f*)(slab + (int64_t)m * N + n) = acc[i][j] * args.alpha;
+      }
+    }
+    return;
+  }
   const float alpha = args.alpha, beta = args.beta;
   const float* __restrict__ bias = args.bias;
   float csum[4][4];
@@ -293,12 +311,36 @@ gemm_kernel(const maeclip_gemm_args args) {
   }
 }
 
+// C[z] = sum_s slab[z][s] (+bias) (+beta*C), fixed summation order
+template <typename OutT>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const maeclip_gemm_args a) {
+  const int64_t MN = a.M * a.N;
+  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e >= MN) return;
+  const int64_t z = blockIdx.y;
+  const float* ws = a.workspace + z * a.splitk * MN + e;
+  v4f v = *(const v4f*)ws;
+  for (int s = 1; s < a.splitk; ++s) v += *(const v4f*)(ws + s * MN);
+  const int64_t m = e / a.N, n = e % a.N;
+  if (a.bias) v += *(const v4f*)(a.bias + n);
+  OutT* cp = (OutT*)a.C + z * a.strideC + m * a.ldc + n;
+  if (a.beta != 0.f) v += a.beta * ld4<OutT>(cp);
+  st4<OutT>(cp, v);
+}
+
 template <typename T, typename OutT, int LA, int LB, int EPI>
 int launch(const maeclip_gemm_args& a, hipStream_t s) {
   const int gm = (int)((a.M + BM - 1) / BM), gn = (int)((a.N + BN - 1) / BN);
-  dim3 grid(gm * gn, 1, (unsigned)a.batch);
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  dim3 grid(gm * gn, S, (unsigned)a.batch);
   hipLaunchKernelGGL((gemm_kernel<T, OutT, LA, LB, EPI>), grid, dim3(NT), 4 * TILE_BYTES, s, a);
   MC_CHECK_LAUNCH("maeclip_gemm");
+  if (S > 1) {
+    const int64_t MN = a.M * a.N;
+    dim3 g2((unsigned)((MN / 4 + 255) / 256), (unsigned)a.batch);
+    hipLaunchKernelGGL((splitk_reduce_kernel<OutT>), g2, dim3(256), 0, s, a);
+    MC_CHECK_LAUNCH("maeclip_gemm(splitk reduce)");
+  }
   return 0;
 }
 
@@ -345,6 +387,11 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   MC_CHECK_ARG(a->epilogue != EPI_DGELU || a->aux, "maeclip_gemm: DGELU epilogue needs aux");
   MC_CHECK_ARG(a->epilogue != EPI_RESID || (a->resid && a->out_dtype == MAECLIP_F32),
                "maeclip_gemm: RESID epilogue needs fp32 resid and fp32 output");
+  if (a->splitk > 1) {
+    MC_CHECK_ARG(a->workspace && a->epilogue == EPI_NONE && !a->colsum_partial && a->splitk <= 64,
+                 "maeclip_gemm: split-K needs a workspace, epilogue 0 and no colsum");
+    MC_CHECK_ARG(a->ldc == a->N, "maeclip_gemm: split-K output must be dense (ldc == N)");
+  }
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);
@@ -352,3 +399,15 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 }
 
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return ((M + BM - 1) / BM) * 2; }
+
+// Slice count for split-K: aim for ~1024 workgroups (4 waves of 256 CUs at 2
+// blocks/CU... the wgrad shapes of the hot path have only 16-144 output tiles
+// but 12.8k-50k deep K), keeping >= 16 K-tiles of 64 per slice.
+extern "C" int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int64_t s = 1024 / (tiles > 0 ? tiles : 1);
+  const int64_t kmax = K / 1024;
+  if (s > kmax) s = kmax;
+  if (s > 64) s = 64;
+  return (int32_t)(s < 1 ? 1 : s);
+}

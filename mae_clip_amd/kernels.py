@@ -51,15 +51,16 @@ def _call(name, *args):
 # ------------------------------------------------------------------ GEMM
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=EPI_NONE, alpha=1.0, beta=0.0,
          bias=None, aux=None, aux_out=None, ldaux=0, resid=None, ldr=0, colsum=None, batch=1,
-         strides=(0, 0, 0)):
-    _dev(A, B, Cout, bias, aux, aux_out, resid, colsum)
+         strides=(0, 0, 0), splitk=1, workspace=None):
+    _dev(A, B, Cout, bias, aux, aux_out, resid, colsum, workspace)
     if A.dtype != B.dtype:
         raise TypeError("gemm: A and B dtypes differ")
     a = L.GemmArgs(A=A.data_ptr(), B=B.data_ptr(), C=Cout.data_ptr(), M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc,
                    batch=batch, strideA=strides[0], strideB=strides[1], strideC=strides[2],
                    dtype=_dt(A), out_dtype=_dt(Cout), a_layout=a_layout, b_layout=b_layout, epilogue=epilogue,
                    alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
-                   resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum))
+                   resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum), splitk=splitk,
+                   workspace=_ptr(workspace))
     if LAUNCH_HOOK is None:
         _call("maeclip_gemm", C.byref(a), _stream())
     else:
@@ -95,12 +96,14 @@ def linear_dgrad(dy, w, out_dtype=None, epilogue=EPI_NONE, aux=None, resid=None,
     return out
 
 
-def linear_wgrad(dy, x, out=None, beta=0.0):
-    """dW[N,K] = dy[M,N]^T x[M,K]  (fp32)."""
+def linear_wgrad(dy, x, out=None, beta=0.0, bias_grad_out=None):
+    """dW[N,K] = dy[M,N]^T x[M,K]  (fp32), split-K over the token dimension."""
     M, N = dy.shape
     K = x.shape[1]
     out = out if out is not None else torch.empty((N, K), device=dy.device, dtype=torch.float32)
-    gemm(dy, x, out, N, K, M, dy.stride(0), x.stride(0), out.stride(0), RC, RC, beta=beta)
+    S = int(L.lib().maeclip_gemm_splitk(N, K, M)) if out.stride(0) == K else 1
+    ws = torch.empty((S * N * K,), device=dy.device, dtype=torch.float32) if S > 1 else None
+    gemm(dy, x, out, N, K, M, dy.stride(0), x.stride(0), out.stride(0), RC, RC, beta=beta, splitk=S, workspace=ws)
     return out
 
 
@@ -109,7 +112,9 @@ def colsum_reduce(partial, out=None, accumulate=False, scale=1.0):
     _dev(partial)
     P, N = partial.shape
     out = out if out is not None else torch.empty((N,), device=partial.device, dtype=torch.float32)
-    _call("maeclip_colsum_reduce", partial.data_ptr(), P, N, out.data_ptr(), int(accumulate), scale, _stream())
+    scratch = torch.empty(((P + 63) // 64, N), device=partial.device, dtype=torch.float32) if (N > 1 and P > 64) else None
+    _call("maeclip_colsum_reduce", partial.data_ptr(), P, N, out.data_ptr(), int(accumulate), scale, _ptr(scratch),
+          _stream())
     return out
 
 

@@ -172,3 +172,23 @@ def test_mask_ids_is_stable_argsort(dev):
     m = torch.ones(B, L_)
     m[:, :keep] = 0
     assert torch.equal(mask.cpu(), torch.gather(m, 1, ids_r.cpu().long()))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_wgrad_splitk(dev, dtype):
+    M, N, Kd = 20000, 256, 136   # long token dim -> split-K (deterministic slab reduce)
+    dy = _rand((M, N), dtype, dev, seed=41)
+    x = _rand((M, Kd), dtype, dev, seed=42)
+    from mae_clip_amd import _lib
+    assert _lib.lib().maeclip_gemm_splitk(N, Kd, M) > 1
+    dW = K.linear_wgrad(dy, x)
+    ref = _ref_mm(dy.t(), x)
+    assert (dW.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-5
+    dW2 = K.linear_wgrad(dy, x)
+    assert torch.equal(dW, dW2)  # deterministic
+
+
+def test_colsum_two_pass(dev):
+    part = _rand((1000, 768), torch.float32, dev, seed=43)
+    out = K.colsum_reduce(part)
+    assert (out.double() - part.double().sum(0)).abs().max().item() < 1e-3

@@ -1,0 +1,52 @@
+"""Per-shape GEMM throughput of libmaeclip vs torch.matmul (hipBLASLt) on the
+production shapes of the C2 step (ViT-B/16 MAE+CLIP, B=256)."""
+import sys, os, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from mae_clip_amd import kernels as K
+
+dev = torch.device("cuda")
+E, D = 256 * 50, 256 * 197   # encoder / decoder token rows
+SHAPES = [  # (name, M, N, K, a_layout, b_layout)
+    ("enc qkv fwd", E, 2304, 768, 0, 0), ("enc fc1 fwd", E, 3072, 768, 0, 0), ("enc fc2 fwd", E, 768, 3072, 0, 0),
+    ("enc proj fwd", E, 768, 768, 0, 0), ("dec qkv fwd", D, 1536, 512, 0, 0), ("dec fc1 fwd", D, 2048, 512, 0, 0),
+    ("dec fc2 fwd", D, 512, 2048, 0, 0), ("dec pred fwd", D, 768, 512, 0, 0),
+    ("enc fc2 dgrad", E, 3072, 768, 0, 1), ("enc fc1 dgrad", E, 768, 3072, 0, 1), ("dec fc2 dgrad", D, 2048, 512, 0, 1),
+    ("dec fc1 dgrad", D, 512, 2048, 0, 1),
+    ("enc fc1 wgrad", 3072, 768, E, 1, 1), ("enc fc2 wgrad", 768, 3072, E, 1, 1), ("enc qkv wgrad", 2304, 768, E, 1, 1),
+    ("dec fc1 wgrad", 2048, 512, D, 1, 1), ("dec fc2 wgrad", 512, 2048, D, 1, 1), ("dec qkv wgrad", 1536, 512, D, 1, 1),
+]
+
+
+def mk(rows, cols):
+    return (torch.randn(rows, cols, device=dev) * 0.5).to(torch.bfloat16)
+
+
+def time_fn(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps / 1e3
+
+
+res = []
+for name, M, N, Kd, la, lb in SHAPES:
+    A = mk(M, Kd) if la == 0 else mk(Kd, M)
+    B = mk(N, Kd) if lb == 0 else mk(Kd, N)
+    C = torch.empty(M, N, device=dev, dtype=torch.float32 if (la, lb) == (1, 1) else torch.bfloat16)
+    f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, la, lb)
+    t = time_fn(f)
+    At = A if la == 0 else A.t()
+    Bt = B.t() if lb == 0 else B
+    tt = time_fn(lambda: torch.matmul(At, Bt))
+    fl = 2.0 * M * N * Kd
+    r = dict(name=name, M=M, N=N, K=Kd, ours_tflops=round(fl / t / 1e12, 1), hipblaslt_tflops=round(fl / tt / 1e12, 1),
+             ours_us=round(t * 1e6, 1))
+    res.append(r)
+    print(json.dumps(r), flush=True)
