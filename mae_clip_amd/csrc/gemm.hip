@@ -26,6 +26,11 @@
 //   output row -> vectorised epilogue loads/stores along N.
 #include "common.h"
 #include "../../include/maeclip.h"
+#include <stdlib.h>
+
+namespace maeclip {
+int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
+}
 
 namespace {
 
@@ -300,8 +305,9 @@ gemm_kernel(const maeclip_gemm_args args) {
         s += __shfl_xor(s, 8, 64);
         csum[j][r] = s;
       }
-    if ((lane & 15) == 0) {
-      float* prow = args.colsum_partial + ((int64_t)z * gm * 2 + bm * 2 + wm) * N;
+    const int mrow = m0 + wm * 64;
+    if ((lane & 15) == 0 && mrow < M) {  // one partial row per 64-row group
+      float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + wn * 64 + 16 * j + 4 * g;
@@ -393,12 +399,17 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
     MC_CHECK_ARG(a->ldc == a->N, "maeclip_gemm: split-K output must be dense (ldc == N)");
   }
   hipStream_t s = (hipStream_t)stream;
+  // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
+  static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
+  if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+      (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
+    return maeclip::gemm_v2(*a, s, forced);
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);
   return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<float, bf16_t>(*a, s) : dispatch_lay<float, float>(*a, s);
 }
 
-extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return ((M + BM - 1) / BM) * 2; }
+extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
 
 // Slice count for split-K: aim for ~1024 workgroups (4 waves of 256 CUs at 2
 // blocks/CU... the wgrad shapes of the hot path have only 16-144 output tiles

@@ -40,7 +40,13 @@ for name, M, N, Kd, la, lb in SHAPES:
     A = mk(M, Kd) if la == 0 else mk(Kd, M)
     B = mk(N, Kd) if lb == 0 else mk(Kd, N)
     C = torch.empty(M, N, device=dev, dtype=torch.float32 if (la, lb) == (1, 1) else torch.bfloat16)
-    f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, la, lb)
+    S = 1
+    ws = None
+    if (la, lb) == (1, 1):  # production wgrad path: deterministic split-K
+        from mae_clip_amd import _lib
+        S = int(_lib.lib().maeclip_gemm_splitk(M, N, Kd))
+        ws = torch.empty(S * M * N, device=dev) if S > 1 else None
+    f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, la, lb, splitk=S, workspace=ws)
     t = time_fn(f)
     At = A if la == 0 else A.t()
     Bt = B.t() if lb == 0 else B
