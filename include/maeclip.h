@@ -160,6 +160,19 @@ int32_t maeclip_ln_bwd_partial_rows(int64_t M);
  * two passes when P > 64 (scratch: f32 [ceil(P/64)][N], may be NULL otherwise) */
 int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate, float scale,
                               float* scratch, void* stream);
+/* many independent column reductions in one launch (bias / LN-parameter
+ * gradients of a whole transformer stack): out[n] (+)= scale * sum_p partial[p][n];
+ * block_start = prefix sum of ceil(N/64) over the entries. */
+typedef struct {
+  const float* partial;
+  float* out;
+  int64_t P, N;
+  float scale;
+  int32_t accumulate;
+  int64_t block_start;
+} maeclip_colsum_entry;
+int32_t maeclip_colsum_multi(const maeclip_colsum_entry* dev_entries, const maeclip_colsum_entry* host_entries,
+                             int32_t ne, void* stream);
 /* partial column sums of a [M, D] row matrix (dtype f32/bf16, row stride ld)
  * into partial [maeclip_rows_colsum_partial_rows(M)][D]; optional bf16 copy
  * out_bf16 [M, D]. */

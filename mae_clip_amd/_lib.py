@@ -59,6 +59,11 @@ class MtEntry(C.Structure):
                 ("n", c_i64), ("chunk_start", c_i64)]
 
 
+class ColsumEntry(C.Structure):
+    _fields_ = [("partial", c_vp), ("out", c_vp), ("P", c_i64), ("N", c_i64), ("scale", c_f32), ("accumulate", c_i32),
+                ("block_start", c_i64)]
+
+
 class AdamwHparams(C.Structure):
     _fields_ = [("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("weight_decay", c_f32),
                 ("step_size", c_f32), ("bc2_sqrt", c_f32), ("grad_scale", c_f32)]
@@ -123,6 +128,7 @@ _SIGS = {
     "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp]),
     "maeclip_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp]),
     "maeclip_mt_chunk": (c_i64, []),
+    "maeclip_colsum_multi": (c_i32, [c_vp, C.POINTER(ColsumEntry), c_i32, c_vp]),
     "maeclip_cast_multi": (c_i32, [c_vp, C.POINTER(MtEntry), c_i32, c_vp]),
     "maeclip_adamw_multi": (c_i32, [c_vp, C.POINTER(MtEntry), c_i32, C.POINTER(AdamwHparams), c_vp]),
     "maeclip_mask_ids": (c_i32, [C.POINTER(MaskArgs), c_vp]),

@@ -158,6 +158,38 @@ int rows_colsum_grid(int64_t M) {
   return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
 }
 
+// Many column reductions in ONE launch: block -> (entry, 64-column chunk),
+// 4 row phases x 64 columns, fixed summation order.
+__global__ void __launch_bounds__(NTH) colsum_multi_kernel(const maeclip_colsum_entry* __restrict__ e, int ne) {
+  __shared__ float red[4][64];
+  int lo = 0, hi = ne - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (e[mid].block_start <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const maeclip_colsum_entry en = e[lo];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int64_t n = (blockIdx.x - en.block_start) * 64 + c;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (n < en.N) {
+    const float* p = en.partial + n;
+    int64_t r = ph;
+    for (; r + 12 < en.P; r += 16) {
+      s0 += p[r * en.N];
+      s1 += p[(r + 4) * en.N];
+      s2 += p[(r + 8) * en.N];
+      s3 += p[(r + 12) * en.N];
+    }
+    for (; r < en.P; r += 4) s0 += p[r * en.N];
+  }
+  red[ph][c] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ph == 0 && n < en.N) {
+    const float v = ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) * en.scale;
+    en.out[n] = en.accumulate ? en.out[n] + v : v;
+  }
+}
+
 // ---- multi-tensor: one block per CHUNK elements, entries located by binary search
 constexpr int64_t CHUNK = 4096;
 
@@ -222,6 +254,15 @@ int64_t mt_blocks(const maeclip_mt_entry* host_entries, int ne) {
 }  // namespace
 
 extern "C" int64_t maeclip_mt_chunk(void) { return CHUNK; }
+
+extern "C" int32_t maeclip_colsum_multi(const maeclip_colsum_entry* dev_entries, const maeclip_colsum_entry* host_entries,
+                                        int32_t ne, void* stream) {
+  MC_CHECK_ARG(dev_entries && host_entries && ne > 0, "maeclip_colsum_multi: bad args");
+  const int64_t nb = host_entries[ne - 1].block_start + (host_entries[ne - 1].N + 63) / 64;
+  hipLaunchKernelGGL(colsum_multi_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, dev_entries, ne);
+  MC_CHECK_LAUNCH("maeclip_colsum_multi");
+  return 0;
+}
 
 extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate,
                                          float scale, float* scratch, void* stream) {

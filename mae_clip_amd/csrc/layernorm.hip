@@ -24,10 +24,10 @@ namespace {
 constexpr int NTH = 256;
 constexpr int MAXC = 8;  // chunks of 4 elements per lane -> D <= 2048
 
-template <typename T>
-__device__ __forceinline__ void load_row(float (&v)[MAXC][4], const T* p, int D, int lane) {
+template <int NC, typename T>
+__device__ __forceinline__ void load_row(float (&v)[NC][4], const T* p, int D, int lane) {
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int e = c * 256 + lane * 4;
     if (e < D) {
       v4f t = ld4<T>(p + e);
@@ -42,39 +42,39 @@ __device__ __forceinline__ float keepf(uint64_t seed, int64_t row, int col, uint
   return mc_hash4(seed, (uint64_t)row, (uint64_t)col, 0x4c4eull) >= thr ? sc : 0.f;
 }
 
-template <typename XT, typename YT>
+template <int NC, typename XT, typename YT>
 __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (NTH / 64) + (threadIdx.x >> 6);
   if (row >= a.M) return;
   const int D = (int)a.D;
-  float v[MAXC][4];
-  load_row<XT>(v, (const XT*)a.x + row * a.ldx, D, lane);
+  float v[NC][4];
+  load_row<NC, XT>(v, (const XT*)a.x + row * a.ldx, D, lane);
   if (a.in_dropout_p > 0.f) {
     const uint32_t thr = (uint32_t)((double)a.in_dropout_p * 4294967296.0);
     const float sc = 1.f / (1.f - a.in_dropout_p);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[c][j] *= keepf(a.seed_in, row, c * 256 + lane * 4 + j, thr, sc);
   }
   if (a.res) {
-    float r[MAXC][4];
-    load_row<float>(r, a.res + row * a.ldres, D, lane);
+    float r[NC][4];
+    load_row<NC, float>(r, a.res + row * a.ldres, D, lane);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[c][j] += r[c][j];
   }
   float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 4; ++j) s += v[c][j];
   const float mean = wave_sum(s) / D;
   float ss = 0.f;
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     if (c * 256 + lane * 4 < D) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { const float d = v[c][j] - mean; ss += d * d; }
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
   const uint32_t othr = (uint32_t)((double)a.out_dropout_p * 4294967296.0);
   const float osc = odrop ? 1.f / (1.f - a.out_dropout_p) : 1.f;
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int e = c * 256 + lane * 4;
     if (e >= D) continue;
     if (a.xsum_out) *(v4f*)(a.xsum_out + row * a.ldxs + e) = v4f{v[c][0], v[c][1], v[c][2], v[c][3]};
@@ -106,28 +106,28 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
   }
 }
 
-template <typename GT, typename XT>
+template <int NC, typename GT, typename XT>
 __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a) {
-  __shared__ float red[NTH / 64][MAXC * 256];
+  __shared__ float red[NTH / 64][NC * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int D = (int)a.D;
-  float pg[MAXC][4], pb[MAXC][4], pc[MAXC][4];
+  float pg[NC][4], pb[NC][4], pc[NC][4];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 4; ++j) pg[c][j] = pb[c][j] = pc[c][j] = 0.f;
 
-  float gm[MAXC][4];
-  load_row<float>(gm, a.gamma, D, lane);
+  float gm[NC][4];
+  load_row<NC, float>(gm, a.gamma, D, lane);
 
   for (int64_t row = (int64_t)blockIdx.x * (NTH / 64) + wave; row < a.M; row += (int64_t)gridDim.x * (NTH / 64)) {
-    float dy[MAXC][4], x[MAXC][4];
-    load_row<GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
-    load_row<XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
+    float dy[NC][4], x[NC][4];
+    load_row<NC, GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
+    load_row<NC, XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
     const float mean = a.mean[row], rstd = a.rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float xh = (x[c][j] - mean) * rstd;
@@ -140,10 +140,10 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
       }
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
-    float dr[MAXC][4];
-    if (a.dres) load_row<float>(dr, a.dres + row * a.lddx, D, lane);
+    float dr[NC][4];
+    if (a.dres) load_row<NC, float>(dr, a.dres + row * a.lddx, D, lane);
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const int e = c * 256 + lane * 4;
       if (e >= D) continue;
       v4f o;
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
   for (int w = 0; w < 3; ++w) {
     if (!outs[w]) continue;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int e = c * 256 + lane * 4 + j;
@@ -194,11 +194,17 @@ extern "C" int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* a, void* stream) {
   if (a->M == 0) return 0;
   dim3 grid((unsigned)((a->M + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-  const bool xb = a->x_dtype == MAECLIP_BF16, yb = a->y_dtype == MAECLIP_BF16;
-  if (xb && yb) hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);
-  else if (xb) hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, float>), grid, dim3(NTH), 0, s, *a);
-  else if (yb) hipLaunchKernelGGL((ln_fwd_kernel<float, bf16_t>), grid, dim3(NTH), 0, s, *a);
-  else hipLaunchKernelGGL((ln_fwd_kernel<float, float>), grid, dim3(NTH), 0, s, *a);
+  const int nc = (int)((a->D + 255) / 256);
+  const int code = (a->x_dtype == MAECLIP_BF16 ? 2 : 0) + (a->y_dtype == MAECLIP_BF16 ? 1 : 0);
+#define LNF(NCV)                                                                                         \
+  case NCV:                                                                                              \
+    if (code == 3) hipLaunchKernelGGL((ln_fwd_kernel<NCV, bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);  \
+    else if (code == 2) hipLaunchKernelGGL((ln_fwd_kernel<NCV, bf16_t, float>), grid, dim3(NTH), 0, s, *a); \
+    else if (code == 1) hipLaunchKernelGGL((ln_fwd_kernel<NCV, float, bf16_t>), grid, dim3(NTH), 0, s, *a); \
+    else hipLaunchKernelGGL((ln_fwd_kernel<NCV, float, float>), grid, dim3(NTH), 0, s, *a);              \
+    break;
+  switch (nc) { LNF(1) LNF(2) LNF(3) LNF(4) LNF(5) LNF(6) LNF(7) LNF(8) }
+#undef LNF
   MC_CHECK_LAUNCH("maeclip_ln_fwd");
   return 0;
 }
@@ -211,11 +217,17 @@ extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
   if (a->M == 0) return 0;
   dim3 grid((unsigned)ln_bwd_grid(a->M));
   hipStream_t s = (hipStream_t)stream;
-  const bool gb = a->dy_dtype == MAECLIP_BF16, xb = a->x_dtype == MAECLIP_BF16;
-  if (gb && xb) hipLaunchKernelGGL((ln_bwd_kernel<bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);
-  else if (gb) hipLaunchKernelGGL((ln_bwd_kernel<bf16_t, float>), grid, dim3(NTH), 0, s, *a);
-  else if (xb) hipLaunchKernelGGL((ln_bwd_kernel<float, bf16_t>), grid, dim3(NTH), 0, s, *a);
-  else hipLaunchKernelGGL((ln_bwd_kernel<float, float>), grid, dim3(NTH), 0, s, *a);
+  const int nc = (int)((a->D + 255) / 256);
+  const int code = (a->dy_dtype == MAECLIP_BF16 ? 2 : 0) + (a->x_dtype == MAECLIP_BF16 ? 1 : 0);
+#define LNB(NCV)                                                                                         \
+  case NCV:                                                                                              \
+    if (code == 3) hipLaunchKernelGGL((ln_bwd_kernel<NCV, bf16_t, bf16_t>), grid, dim3(NTH), 0, s, *a);  \
+    else if (code == 2) hipLaunchKernelGGL((ln_bwd_kernel<NCV, bf16_t, float>), grid, dim3(NTH), 0, s, *a); \
+    else if (code == 1) hipLaunchKernelGGL((ln_bwd_kernel<NCV, float, bf16_t>), grid, dim3(NTH), 0, s, *a); \
+    else hipLaunchKernelGGL((ln_bwd_kernel<NCV, float, float>), grid, dim3(NTH), 0, s, *a);              \
+    break;
+  switch (nc) { LNB(1) LNB(2) LNB(3) LNB(4) LNB(5) LNB(6) LNB(7) LNB(8) }
+#undef LNB
   MC_CHECK_LAUNCH("maeclip_ln_bwd");
   return 0;
 }

@@ -83,6 +83,7 @@ class TransformerStackFn(torch.autograd.Function):
         M = B * n
         params = ctx.params
         grads = [None] * len(params)
+        rb = K.ReduceBatch()
         g = gy.reshape(M, D)
         if not g.is_contiguous():
             g = g.contiguous()
@@ -97,39 +98,40 @@ class TransformerStackFn(torch.autograd.Function):
             xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, pre, a = ctx.saved[i]
             gi = [None] * PER_BLOCK
             # mlp.fc2 (+ GELU backward fused into the dgrad epilogue)
-            gi[11] = _reduce(cpart)
+            gi[11] = rb.add(cpart)
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
             dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_DGELU, aux=pre, colsum=dA_part)
             gi[10] = K.linear_wgrad(gT, a)
             del a, pre
             # mlp.fc1
-            gi[9] = _reduce(dA_part)
+            gi[9] = rb.add(dA_part)
             dh2 = K.linear_dgrad(dA, w1)
             gi[8] = K.linear_wgrad(dA, h2)
             del dA
             # norm2 (+ residual gradient)
             dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True)
-            gi[6], gi[7] = _reduce(pg), _reduce(pb)
+            gi[6], gi[7] = rb.add(pg), rb.add(pb)
             if not bf:
                 dx1T = dx1
             # attn.proj
-            gi[5] = _reduce(pc)
+            gi[5] = rb.add(pc)
             dO = K.linear_dgrad(dx1T, wproj)
             gi[4] = K.linear_wgrad(dx1T, o)
             # attention
             dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
             del dO
-            gi[3] = _reduce(qpart)
+            gi[3] = rb.add(qpart)
             dh1 = K.linear_dgrad(dqkv, wqkv)
             gi[2] = K.linear_wgrad(dqkv, h1)
             del dqkv
             # norm1 (+ residual gradient)
             dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True)
-            gi[0], gi[1] = _reduce(pg), _reduce(pb)
+            gi[0], gi[1] = rb.add(pg), rb.add(pb)
             ctx.saved[i] = None
             g, gT, cpart = dx, (dxT if bf else dx), pc
             for j in range(PER_BLOCK):
                 grads[i * PER_BLOCK + j] = gi[j].view(p[j].shape)
+        rb.flush()
         ctx.saved = None
         return (g.view(B, n, D), None, *grads)
 

@@ -337,6 +337,65 @@ def clip_loss(I, T, temperature, want_grad=True):
 
 
 # ------------------------------------------------------------ multi-tensor
+class PinnedStager:
+    """Host -> device staging of small descriptor arrays through a ring of pinned
+    buffers; a buffer is reused only after the async copy that read it is done."""
+
+    def __init__(self, slots=4):
+        self.bufs = [None] * slots
+        self.events = [None] * slots
+        self.k = 0
+
+    def stage(self, host_struct_array, device):
+        nbytes = C.sizeof(host_struct_array)
+        k = self.k
+        self.k = (k + 1) % len(self.bufs)
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        buf = self.bufs[k]
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 4096), dtype=torch.uint8).pin_memory()
+            self.bufs[k] = buf
+        buf[:nbytes].numpy()[:] = memoryview(host_struct_array).cast("B")
+        dev = buf[:nbytes].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return dev
+
+
+_STAGER = PinnedStager()
+
+
+class ReduceBatch:
+    """Collects column reductions and runs them as ONE maeclip_colsum_multi launch."""
+
+    def __init__(self):
+        self.items = []
+
+    def add(self, partial, scale=1.0):
+        P, N = partial.shape
+        out = torch.empty((N,), device=partial.device, dtype=torch.float32)
+        self.items.append((partial, out, scale))
+        return out
+
+    def flush(self):
+        if not self.items:
+            return
+        n = len(self.items)
+        host = (L.ColsumEntry * n)()
+        start = 0
+        for i, (part, out, scale) in enumerate(self.items):
+            h = host[i]
+            h.partial, h.out = part.data_ptr(), out.data_ptr()
+            h.P, h.N = part.shape
+            h.scale, h.accumulate, h.block_start = scale, 0, start
+            start += (part.shape[1] + 63) // 64
+        dev = _STAGER.stage(host, self.items[0][0].device)
+        _call("maeclip_colsum_multi", dev.data_ptr(), host, n, _stream())
+        self.items = []
+
+
 class MultiTensorPlan:
     """Host + device entry arrays for one multi-tensor launch."""
 
