@@ -30,6 +30,7 @@
 
 namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
+int gemm_v3(const maeclip_gemm_args& a, hipStream_t s);
 }
 
 namespace {
@@ -401,9 +402,12 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
+  if (a->dtype == MAECLIP_BF16 && forced == 5 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+      a->M >= 256 && a->N >= 256)
+    return maeclip::gemm_v3(*a, s);
   if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
       (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
-    return maeclip::gemm_v2(*a, s, forced);
+    return maeclip::gemm_v2(*a, s, forced == 5 ? 0 : forced);
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);
   return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<float, bf16_t>(*a, s) : dispatch_lay<float, float>(*a, s);

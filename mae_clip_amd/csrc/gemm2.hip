@@ -161,11 +161,20 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const maeclip_gemm_
   OutT* __restrict__ C = (OutT*)args.C + z * args.strideC;
   const float alpha = args.alpha, beta = args.beta;
   const float* __restrict__ bias = args.bias;
-  float csum[FN][4];
+  constexpr int NH = TM / 64;  // 64-row groups per wave (column-sum partial rows)
+  float csum[NH][FN][4];
 #pragma unroll
-  for (int j = 0; j < FN; ++j)
+  for (int hh = 0; hh < NH; ++hh)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csum[hh][j][r] = 0.f;
+  v4f bias4[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = min(n0 + wn * TN + 16 * j + 4 * g, N - 4);
+    bias4[j] = bias ? *(const v4f*)(bias + n) : v4f{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm * TM + 16 * i + (lane & 15);
@@ -174,8 +183,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const maeclip_gemm_
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + wn * TN + 16 * j + 4 * g;
       if (!mok || n >= N) continue;
-      v4f v = acc[i][j] * alpha;
-      if (bias) v += *(const v4f*)(bias + n);
+      v4f v = acc[i][j] * alpha + bias4[j];
       if (EPI == EPI_GELU) {
         st4<bf16_t>((bf16_t*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, v);
 #pragma unroll
@@ -191,29 +199,32 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const maeclip_gemm_
       OutT* cp = C + (int64_t)m * args.ldc + n;
       if (beta != 0.f) v += beta * ld4<OutT>(cp);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) csum[j][r] += v[r];
+      for (int r = 0; r < 4; ++r) csum[i / 4][j][r] += v[r];
       st4<OutT>(cp, v);
     }
   }
-  if (args.colsum_partial) {  // one partial row per 64-row group (TM == 64)
+  if (args.colsum_partial) {  // one partial row per 64-row group
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = csum[j][r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        csum[j][r] = s;
-      }
-    const int mrow = m0 + wm * TM;
-    if ((lane & 15) == 0 && mrow < M) {
-      float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N;
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * TN + 16 * j + 4 * g;
-        if (n < N) *(v4f*)(prow + n) = v4f{csum[j][0], csum[j][1], csum[j][2], csum[j][3]};
+        for (int r = 0; r < 4; ++r) {
+          float s = csum[hh][j][r];
+          s += __shfl_xor(s, 1, 64);
+          s += __shfl_xor(s, 2, 64);
+          s += __shfl_xor(s, 4, 64);
+          s += __shfl_xor(s, 8, 64);
+          csum[hh][j][r] = s;
+        }
+      const int mrow = m0 + wm * TM + 64 * hh;
+      if ((lane & 15) == 0 && mrow < M) {
+        float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = n0 + wn * TN + 16 * j + 4 * g;
+          if (n < N) *(v4f*)(prow + n) = v4f{csum[hh][j][0], csum[hh][j][1], csum[hh][j][2], csum[hh][j][3]};
+        }
       }
     }
   }
@@ -269,6 +280,8 @@ int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant) {
     case 2: return lay2<256, 128, 4, 2>(a, s);
     case 3: return lay2<128, 256, 2, 4>(a, s);
     case 4: return lay2<256, 256, 4, 4>(a, s);
+    case 6: return lay2<256, 256, 2, 4>(a, s);
+    case 7: return lay2<256, 128, 2, 2>(a, s);
     default: return lay2<128, 128, 2, 2>(a, s);
   }
 }
