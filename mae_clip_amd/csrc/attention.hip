@@ -32,8 +32,9 @@
 
 namespace {
 
-constexpr int NW = 8;            // waves per workgroup
-constexpr int NTH = NW * 64;
+constexpr int MAXW = 8;          // max waves per workgroup (sized per launch to the tile count)
+#define NW ((int)(blockDim.x >> 6))
+#define NTH ((int)blockDim.x)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
 
@@ -156,7 +157,7 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t bh, int q, 
 
 // ============================================================== forward
 template <typename T, int HD>
-__global__ void __launch_bounds__(NTH) attn_fwd_kernel(const maeclip_attn_args a) {
+__global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
@@ -265,7 +266,7 @@ __global__ void __launch_bounds__(NTH) attn_fwd_kernel(const maeclip_attn_args a
 
 // ============================================================== backward
 template <typename T, int HD>
-__global__ void __launch_bounds__(NTH) attn_bwd_kernel(const maeclip_attn_args a) {
+__global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
@@ -452,22 +453,26 @@ template <typename T, int HD> size_t fwd_lds(int n) {
   const int npad = (n + 63) & ~63;
   return (size_t)2 * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
 }
-template <typename T, int HD> size_t bwd_lds(int n) {
+template <typename T, int HD> size_t bwd_lds(int n, int nw) {
   const int npad = (n + 31) & ~31;
-  return (size_t)4 * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)NW * 3 * HD * 4;
+  return (size_t)4 * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
 template <typename T, int HD>
 int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
-  const size_t lds = bwd ? bwd_lds<T, HD>(a.n) : fwd_lds<T, HD>(a.n);
+  // one wave per 16-row tile (no idle waves), at most MAXW
+  const int tiles = (a.n + 15) / 16;
+  const int nw = tiles < MAXW ? tiles : MAXW;
+  const int nthreads = 64 * nw;
+  const size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   dim3 grid((unsigned)(a.B * a.H));
   if (bwd) {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((attn_bwd_kernel<T, HD>), grid, dim3(NTH), lds, s, a);
+    hipLaunchKernelGGL((attn_bwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);
   } else {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(NTH), lds, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);
   }
   MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");
   return 0;
