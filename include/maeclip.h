@@ -47,7 +47,12 @@ int32_t maeclip_device_count(void);
  * (A[k*lda+m], B[k*ldb+n]).
  * epilogue: 0 none; 1 GELU (aux_out <- pre-activation, C <- gelu(pre));
  *           2 residual (C(f32) <- resid + acc (+bias)); 3 dGELU (C <- acc *
- *           gelu'(aux) (+ resid if resid != NULL)).
+ *           gelu'(aux) (+ resid if resid != NULL)); 4 GELU' (C <- gelu(pre),
+ *           aux_out <- gelu'(pre): the backward then needs no transcendental);
+ *           5 mul-aux (C <- acc * aux (+ resid if resid != NULL)).
+ *           For 1 and 4 aux_out may be NULL (forward-only callers).
+ *           aux / aux_out have the operand dtype on the fp32 path, bf16 on the
+ *           bf16 path.
  * colsum_partial (optional, f32 [batch*maeclip_gemm_colsum_rows(M)][N]):
  *   per-block column sums of the final C, reduce with maeclip_colsum_reduce.
  * splitk > 1 (epilogue 0, no colsum): K is cut into splitk slices whose fp32

@@ -91,14 +91,45 @@ template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, v4f v) {
   *(v2u*)p = u;
 }
 
-// exact (erf) GELU, as nn.GELU() / HF "gelu" / timm default
+// erf-GELU (nn.GELU() / HF "gelu" / timm default) and its derivative sharing
+// one exp: Phi(x) = 0.5 erfc(-x/sqrt2) with erfc by Abramowitz & Stegun 7.1.26
+// (|err| <= 1.5e-7; |gelu err| <= 4.2e-7 over [-12,12], the same as f32 erff),
+// phi(x) = exp(-x^2/2)/sqrt(2 pi). The tail is taken from erfc directly, so
+// gelu(x) for x << 0 has no cancellation.
+__device__ __forceinline__ void gelu_pair(float x, float& y, float& dy) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float e = __expf(-0.5f * x * x);
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float ht = 0.5f * p * t * e;           // 0.5 erfc(|x|/sqrt2)
+  const float cdf = x < 0.f ? ht : 1.0f - ht;
+  y = x * cdf;
+  dy = fmaf(x * e, 0.39894228040143268f, cdf);
+}
+// gelu and gelu' of the 4 lanes of v: v <- gelu(v), returns gelu'(v)
+__device__ __forceinline__ v4f gelu4_inplace(v4f& v) {
+  v4f d;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float y, dy;
+    gelu_pair(v[r], y, dy);
+    v[r] = y;
+    d[r] = dy;
+  }
+  return d;
+}
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  float y, dy;
+  gelu_pair(x, y, dy);
+  return y;
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float y, dy;
+  gelu_pair(x, y, dy);
+  return dy;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

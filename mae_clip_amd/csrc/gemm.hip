@@ -31,6 +31,8 @@
 namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v3(const maeclip_gemm_args& a, hipStream_t s);
+int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
+bool gemm_v4_ok(const maeclip_gemm_args& a);
 }
 
 namespace {
@@ -39,7 +41,7 @@ constexpr int BM = 128, BN = 128, NT = 256;
 constexpr int TILE_BYTES = 16384;  // one operand, one stage
 
 enum { LAY_KC = 0, LAY_RC = 1 };
-enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3 };
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3, EPI_GELU_D = 4, EPI_MUL_AUX = 5 };
 
 template <typename T> struct Tr;
 template <> struct Tr<bf16_t> { static constexpr int BK = 64; static constexpr int EPC = 8; };
@@ -274,7 +276,7 @@ gemm_kernel(const maeclip_gemm_args args) {
         v += bb;
       }
       if (EPI == EPI_GELU) {
-        st4<T>((T*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, v);
+        if (args.aux_out) st4<T>((T*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, v);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
       } else if (EPI == EPI_RESID) {
@@ -283,6 +285,12 @@ gemm_kernel(const maeclip_gemm_args args) {
         const v4f pre = ld4<T>((const T*)args.aux + z * args.strideC + (int64_t)m * args.ldaux + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_f(pre[r]);
+        if (args.resid) v += *(const v4f*)(args.resid + z * args.strideC + (int64_t)m * args.ldr + n);
+      } else if (EPI == EPI_GELU_D) {
+        const v4f d = gelu4_inplace(v);
+        if (args.aux_out) st4<T>((T*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, d);
+      } else if (EPI == EPI_MUL_AUX) {
+        v *= ld4<T>((const T*)args.aux + z * args.strideC + (int64_t)m * args.ldaux + n);
         if (args.resid) v += *(const v4f*)(args.resid + z * args.strideC + (int64_t)m * args.ldr + n);
       }
       OutT* cp = C + (int64_t)m * args.ldc + n;
@@ -358,6 +366,8 @@ int dispatch_epi(const maeclip_gemm_args& a, hipStream_t s) {
     case EPI_GELU: return launch<T, OutT, LA, LB, EPI_GELU>(a, s);
     case EPI_RESID: return launch<T, OutT, LA, LB, EPI_RESID>(a, s);
     case EPI_DGELU: return launch<T, OutT, LA, LB, EPI_DGELU>(a, s);
+    case EPI_GELU_D: return launch<T, OutT, LA, LB, EPI_GELU_D>(a, s);
+    case EPI_MUL_AUX: return launch<T, OutT, LA, LB, EPI_MUL_AUX>(a, s);
   }
   maeclip::set_error("maeclip_gemm: bad epilogue %d", a.epilogue);
   return -1;
@@ -390,8 +400,8 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   MC_CHECK_ARG(a->N % 4 == 0 && a->ldc % 4 == 0, "maeclip_gemm: N and ldc must be multiples of 4");
   MC_CHECK_ARG(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && ((uintptr_t)a->C & 7) == 0,
                "maeclip_gemm: operands must be 16-byte aligned");
-  MC_CHECK_ARG(a->epilogue != EPI_GELU || a->aux_out, "maeclip_gemm: GELU epilogue needs aux_out");
-  MC_CHECK_ARG(a->epilogue != EPI_DGELU || a->aux, "maeclip_gemm: DGELU epilogue needs aux");
+  MC_CHECK_ARG((a->epilogue != EPI_DGELU && a->epilogue != EPI_MUL_AUX) || a->aux,
+               "maeclip_gemm: DGELU / MUL_AUX epilogue needs aux");
   MC_CHECK_ARG(a->epilogue != EPI_RESID || (a->resid && a->out_dtype == MAECLIP_F32),
                "maeclip_gemm: RESID epilogue needs fp32 resid and fp32 output");
   if (a->splitk > 1) {
@@ -402,12 +412,15 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
-  if (a->dtype == MAECLIP_BF16 && forced == 5 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+  if (a->dtype == MAECLIP_BF16 && forced == 5 && a->epilogue <= EPI_DGELU && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
       a->M >= 256 && a->N >= 256)
     return maeclip::gemm_v3(*a, s);
+  // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
+  // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
+  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a)) return maeclip::gemm_v4(*a, s);
   if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
       (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
-    return maeclip::gemm_v2(*a, s, forced == 5 ? 0 : forced);
+    return maeclip::gemm_v2(*a, s, (forced == 5 || forced == 8) ? 0 : forced);
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);
   return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<float, bf16_t>(*a, s) : dispatch_lay<float, float>(*a, s);

@@ -20,7 +20,7 @@
 namespace {
 
 enum { LAY_KC = 0, LAY_RC = 1 };
-enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3 };
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3, EPI_GELU_D = 4, EPI_MUL_AUX = 5 };
 
 __device__ __forceinline__ int swz_rc(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
 
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const maeclip_gemm_
       if (!mok || n >= N) continue;
       v4f v = acc[i][j] * alpha + bias4[j];
       if (EPI == EPI_GELU) {
-        st4<bf16_t>((bf16_t*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, v);
+        if (args.aux_out) st4<bf16_t>((bf16_t*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, v);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
       } else if (EPI == EPI_RESID) {
@@ -194,6 +194,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const maeclip_gemm_
         const v4f pre = ld4<bf16_t>((const bf16_t*)args.aux + z * args.strideC + (int64_t)m * args.ldaux + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= gelu_grad_f(pre[r]);
+        if (args.resid) v += *(const v4f*)(args.resid + z * args.strideC + (int64_t)m * args.ldr + n);
+      } else if (EPI == EPI_GELU_D) {
+        const v4f d = gelu4_inplace(v);
+        if (args.aux_out) st4<bf16_t>((bf16_t*)args.aux_out + z * args.strideC + (int64_t)m * args.ldaux + n, d);
+      } else if (EPI == EPI_MUL_AUX) {
+        v *= ld4<bf16_t>((const bf16_t*)args.aux + z * args.strideC + (int64_t)m * args.ldaux + n);
         if (args.resid) v += *(const v4f*)(args.resid + z * args.strideC + (int64_t)m * args.ldr + n);
       }
       OutT* cp = C + (int64_t)m * args.ldc + n;
@@ -248,6 +254,8 @@ int epi2(const maeclip_gemm_args& a, hipStream_t s) {
     case EPI_NONE: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_NONE>(a, s);
     case EPI_GELU: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_GELU>(a, s);
     case EPI_RESID: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_RESID>(a, s);
+    case EPI_GELU_D: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_GELU_D>(a, s);
+    case EPI_MUL_AUX: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_MUL_AUX>(a, s);
     default: return launch2<BM, BN, WM, WN, LA, LB, OutT, EPI_DGELU>(a, s);
   }
 }

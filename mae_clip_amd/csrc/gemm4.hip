@@ -1,0 +1,621 @@
+// GEMM v4: 256x256x64 bf16 tile, 8 waves in two ping-pong groups, LDS-DMA
+// prefetch kept in flight across raw barriers (the 256² 8-phase structure of
+// cdna_hip_programming.md §5, restated for this library's operand layouts and
+// epilogues).
+//
+// Geometry: waves (wm, wn) = 2 x 4, each wave owns a 128 x 64 output block as
+// 8 x 4 fragments of 16x16 (acc = 128 VGPRs). A K-tile is split into four
+// 16-KiB "halves" so that each half's last LDS read lands at a different phase:
+//   Am0 = A rows {0-63, 128-191}  (mi = 0 sub-rows of both wave rows)
+//   Am1 = A rows {64-127, 192-255}
+//   Bn0 = B cols {0-31, 64-95, 128-159, 192-223} (ni = 0 sub-cols of all wn)
+//   Bn1 = the other 128 columns
+// Per K-tile every wave runs four phases, each one 64x32 output quadrant x K 64
+// = 16 MFMA 16x16x32:
+//   p0 (mi0,ni0): read A-sub0 + B-sub0     p1 (mi0,ni1): read B-sub1
+//   p2 (mi1,ni1): read A-sub1              p3 (mi1,ni0): B-sub0 still in VGPRs
+// so the last LDS reads are Am0,Bn0 @p0, Bn1 @p1, Am1 @p2.
+// DMA schedule (2 glds per wave per phase = one half):
+//   p0 of tile t issues half Am1 of tile t+1;  p1,p2,p3 issue Am0,Bn0,Bn1 of
+//   tile t+2 into the buffer tile t is still being read -- each one phase after
+//   that half's last read (the reads are retired by lgkmcnt(0) before the
+//   barrier that ends the reading segment).
+//   p3 waits vmcnt(6): everything but the three youngest halves (tile t+2's)
+//   has landed, i.e. all of tile t+1, before the barrier that precedes its
+//   first read.
+// Ping-pong: group 1 (wm == 1) executes one extra barrier up front, so in every
+// barrier-delimited segment one group issues its ds_reads/DMA while the other
+// group's 16 MFMAs run (one wave of each group per SIMD).
+#include "common.h"
+#include "../../include/maeclip.h"
+
+namespace {
+
+enum { LAY_KC = 0, LAY_RC = 1 };
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3, EPI_GELU_D = 4, EPI_MUL_AUX = 5 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int swz_rc(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
+
+#ifdef GEMM4_STAMPS
+__device__ uint64_t g_stamps[256 * 8 * 2 * 4];
+#endif
+
+constexpr int HALF = 16384;          // bytes per half image (128 rows/cols x 64 k x bf16)
+constexpr int BUF = 4 * HALF;        // one K-tile
+constexpr int LDS_BYTES = 2 * BUF;   // 128 KiB
+
+// local index l (0..127) of a half -> offset inside the 256-wide block tile
+__device__ __forceinline__ int amap(int l, int sub) { return (l & 63) + ((l >> 6) << 7) + (sub << 6); }
+__device__ __forceinline__ int bmap(int l, int sub) { return (l & 31) + ((l >> 5) << 6) + (sub << 5); }
+
+// Operand DMA through buffer descriptors (buffer_load_dwordx4 ... lds): the
+// tile base and extent live in SGPRs, the per-lane byte offsets of the two
+// wave-instructions this wave issues per half are loop invariants (8 VGPRs for
+// both operands), and the K-tile advance is the scalar soffset. Rows (KC) past
+// the operand's end read as zero through the descriptor's range check, so no
+// clamping is needed; RC columns past N read neighbouring (finite) data whose
+// results are never stored.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const bf16_t* base, int64_t bytes) {
+  const int nrec = (int)(bytes < 0x7fffffff ? (bytes > 0 ? bytes : 0) : 0x7fffffff);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
+}
+
+// per-lane byte offset of wave-instruction i (0, 1) of half `sub` (0, 1) of an operand
+template <int LAY, bool ISA>
+__device__ __forceinline__ int half_voffset(int64_t ld, int sub, int i, int wave, int lane) {
+  const int q = i * 8 + wave;
+  if (LAY == LAY_KC) {
+    const int r = q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int g = ISA ? amap(r, sub) : bmap(r, sub);
+    return (int)(g * ld * 2) + c * 16;
+  } else {
+    const int kr = q * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ (swz_rc(kr) >> 1);
+    const int g = ISA ? amap(c * 8, sub) : bmap(c * 8, sub);
+    return (int)(kr * ld * 2) + g * 2;
+  }
+}
+
+// One half = 16 wave-instructions of 1 KiB; this wave issues 2 of them.
+__device__ __forceinline__ void issue_half(rsrc_t rs, int v0, int v1, int soff, char* lds, int wave) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + wave * 1024), 16, v0, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + (8 + wave) * 1024), 16, v1, soff, 0, 0);
+}
+
+template <int LAY>
+__device__ __forceinline__ v8s frag(const char* lds, int rs, int ks, int lane) {
+  if (LAY == LAY_KC) {
+    const int row = rs + (lane & 15);
+    const int chunk = 4 * ks + (lane >> 4);
+    return *(const v8s*)(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int unit = (rs >> 2) + p;
+    v8s v;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int krow = 32 * ks + 8 * g + 4 * h + q;
+      const char* a = lds + krow * 256 + ((unit ^ swz_rc(krow)) << 3);
+      v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, a));
+      v[4 * h + 0] = t[0];
+      v[4 * h + 1] = t[1];
+      v[4 * h + 2] = t[2];
+      v[4 * h + 3] = t[3];
+    }
+    return v;
+  }
+}
+
+#define SEG_BARRIER()                        \
+  do {                                       \
+    asm volatile("" ::: "memory");           \
+    __builtin_amdgcn_sched_barrier(0);       \
+    __builtin_amdgcn_s_barrier();            \
+    __builtin_amdgcn_sched_barrier(0);       \
+    asm volatile("" ::: "memory");           \
+  } while (0)
+
+// Epilogue. Fragment (i, j) of the wave covers rows m0 + 128 wm + 64 (i>>2) +
+// 16 (i&3) and columns n0 + 64 wn + 32 (j>>1) + 16 (j&1); the MFMA leaves lane
+// l with C[row l&15][4 (l>>4) .. +3] of each fragment. A permlane16 swap of the
+// column pair (2 ni, 2 ni + 1) hands every lane 8 CONSECUTIVE columns of one
+// fragment (lane group g: fragment g&1, columns 8 (g>>1) .. +7), so a row
+// segment is one 16-B access per lane (bf16) instead of two 8-B ones
+// (cdna_hip_programming.md T21).
+//
+// vmcnt is in-order on CDNA: a load issued after a store can only be waited
+// for together with that store. So every load (bias, aux, resid) of a chunk of
+// two row fragments is issued BEFORE the stores of the previous chunk, and the
+// stores themselves are never waited for here (they drain behind the next
+// tile's main loop, see the counted wait at the tile start).
+__device__ __forceinline__ void swap_pairs(v4f (&acc)[8][4]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * ni][r]),
+                                                  __float_as_uint(acc[i][2 * ni + 1][r]), false, false);
+        acc[i][2 * ni][r] = __uint_as_float(p[0]);
+        acc[i][2 * ni + 1][r] = __uint_as_float(p[1]);
+      }
+}
+
+// split-K slab: fp32 partial of this K slice, no epilogue
+__device__ __forceinline__ void epilogue4_slab(const maeclip_gemm_args& args, v4f (&acc)[8][4], int64_t z, int m0,
+                                               int n0, int wm, int wn, int lane) {
+  const int M = (int)args.M, N = (int)args.N;
+  const int g = lane >> 4;
+  const int S = args.splitk;
+  swap_pairs(acc);
+  float* slab = args.workspace + ((int64_t)z * S + blockIdx.y) * (int64_t)M * N;
+  const float alpha = args.alpha;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + 128 * wm + 64 * (i >> 2) + 16 * (i & 3) + (lane & 15);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int n = n0 + 64 * wn + 32 * ni + 16 * (g & 1) + 8 * (g >> 1);
+      if (m < M && n < N) {
+        float* d = slab + (int64_t)m * N + n;
+        *(v4f*)d = acc[i][2 * ni] * alpha;
+        *(v4f*)(d + 4) = acc[i][2 * ni + 1] * alpha;
+      }
+    }
+  }
+}
+
+template <typename OutT, int EPI>
+__device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&acc)[8][4], int64_t z, int m0, int n0,
+                                          int wm, int wn, int lane) {
+  constexpr bool LOAD_AUX = EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
+  constexpr bool LOAD_RES = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
+  const int M = (int)args.M, N = (int)args.N;
+  const int g = lane >> 4;
+  swap_pairs(acc);
+  const int64_t off = z * args.strideC;
+  OutT* __restrict__ C = (OutT*)args.C + off;
+  const float alpha = args.alpha, beta = args.beta;
+  const bool has_res = LOAD_RES && args.resid != nullptr;
+  const int rbase = m0 + 128 * wm + (lane & 15);
+  const int cb0 = n0 + 64 * wn + 16 * (g & 1) + 8 * (g >> 1);   // + 32 ni
+  v4f bias8[2][2];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = min(cb0 + 32 * ni, N - 8);   // N % 8 == 0 on this path
+    bias8[ni][0] = args.bias ? *(const v4f*)(args.bias + n) : v4f{0.f, 0.f, 0.f, 0.f};
+    bias8[ni][1] = args.bias ? *(const v4f*)(args.bias + n + 4) : v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  // chunk c = row fragment i = c (hh = c >> 2); q = ni
+  v4u ax[2][2];
+  v4f rs[2][2][2];
+  auto load_chunk = [&](int c, int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = c, ni = q;
+      const int m = min(rbase + 64 * (i >> 2) + 16 * (i & 3), M - 1);
+      const int n = min(cb0 + 32 * ni, N - 8);
+      if (LOAD_AUX) ax[buf][q] = *(const v4u*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + n);
+      if (LOAD_RES && has_res) {
+        const float* rp = args.resid + off + (int64_t)m * args.ldr + n;
+        rs[buf][q][0] = *(const v4f*)rp;
+        rs[buf][q][1] = *(const v4f*)(rp + 4);
+      }
+    }
+  };
+  float csum[2][8];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) csum[ni][r] = 0.f;
+  if (LOAD_AUX || LOAD_RES) load_chunk(0, 0);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if ((LOAD_AUX || LOAD_RES) && c + 1 < 8) load_chunk(c + 1, (c + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);   // keep chunk c+1's loads ahead of chunk c's stores
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = c, ni = q;
+      const int m = rbase + 64 * (i >> 2) + 16 * (i & 3);
+      const int n = cb0 + 32 * ni;
+      v4f lo = acc[i][2 * ni] * alpha + bias8[ni][0];
+      v4f hi = acc[i][2 * ni + 1] * alpha + bias8[ni][1];
+      if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
+        v4f dlo = lo, dhi = hi;   // GELU: aux_out <- pre-activation
+        if (EPI == EPI_GELU_D) {
+          dlo = gelu4_inplace(lo);
+          dhi = gelu4_inplace(hi);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lo[r] = gelu_f(lo[r]);
+            hi[r] = gelu_f(hi[r]);
+          }
+        }
+        if (args.aux_out && m < M && n < N) {
+          v4u pk;
+          pk[0] = pack2bf(dlo[0], dlo[1]);
+          pk[1] = pack2bf(dlo[2], dlo[3]);
+          pk[2] = pack2bf(dhi[0], dhi[1]);
+          pk[3] = pack2bf(dhi[2], dhi[3]);
+          *(v4u*)((bf16_t*)args.aux_out + off + (int64_t)m * args.ldaux + n) = pk;
+        }
+      }
+      if (LOAD_AUX) {
+        const v4u pk = ax[c & 1][q];
+        if (EPI == EPI_MUL_AUX) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            lo[2 * r] *= __uint_as_float(pk[r] << 16);
+            lo[2 * r + 1] *= __uint_as_float(pk[r] & 0xffff0000u);
+            hi[2 * r] *= __uint_as_float(pk[2 + r] << 16);
+            hi[2 * r + 1] *= __uint_as_float(pk[2 + r] & 0xffff0000u);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            lo[2 * r] *= gelu_grad_f(__uint_as_float(pk[r] << 16));
+            lo[2 * r + 1] *= gelu_grad_f(__uint_as_float(pk[r] & 0xffff0000u));
+            hi[2 * r] *= gelu_grad_f(__uint_as_float(pk[2 + r] << 16));
+            hi[2 * r + 1] *= gelu_grad_f(__uint_as_float(pk[2 + r] & 0xffff0000u));
+          }
+        }
+      }
+      if (LOAD_RES && has_res) {
+        lo += rs[c & 1][q][0];
+        hi += rs[c & 1][q][1];
+      }
+      if (m < M && n < N) {
+        OutT* cp = C + (int64_t)m * args.ldc + n;
+        if (beta != 0.f) {
+          lo += beta * ld4<OutT>(cp);
+          hi += beta * ld4<OutT>(cp + 4);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          csum[ni][r] += lo[r];
+          csum[ni][4 + r] += hi[r];
+        }
+        if (sizeof(OutT) == 2) {
+          v4u pk;
+          pk[0] = pack2bf(lo[0], lo[1]);
+          pk[1] = pack2bf(lo[2], lo[3]);
+          pk[2] = pack2bf(hi[0], hi[1]);
+          pk[3] = pack2bf(hi[2], hi[3]);
+          *(v4u*)cp = pk;
+        } else {
+          *(v4f*)cp = lo;
+          *(v4f*)((float*)cp + 4) = hi;
+        }
+      }
+    }
+    if ((c & 3) == 3 && args.colsum_partial) {  // one partial row per 64-row group hh = c >> 2
+      const int hh = c >> 2;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float sv = csum[ni][r];
+          sv += __shfl_xor(sv, 1, 64);
+          sv += __shfl_xor(sv, 2, 64);
+          sv += __shfl_xor(sv, 4, 64);
+          sv += __shfl_xor(sv, 8, 64);
+          csum[ni][r] = sv;
+        }
+      const int mrow = m0 + 128 * wm + 64 * hh;
+      if ((lane & 15) == 0 && mrow < M) {
+        float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int n = cb0 + 32 * ni;
+          if (n < N) {
+            *(v4f*)(prow + n) = v4f{csum[ni][0], csum[ni][1], csum[ni][2], csum[ni][3]};
+            *(v4f*)(prow + n + 4) = v4f{csum[ni][4], csum[ni][5], csum[ni][6], csum[ni][7]};
+          }
+        }
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) csum[ni][r] = 0.f;
+    }
+  }
+}
+
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int M = (int)args.M, N = (int)args.N, K = (int)args.K;
+
+  const int gm = (M + 255) / 256, gn = (N + 255) / 256;
+  const int T = gm * gn;
+  // Persistent over output tiles: the tiles are cut into 8 contiguous chunks,
+  // chunk x worked by the blocks with blockIdx.x % 8 == x (round-robin
+  // dispatch puts them on one XCD, so concurrently running tiles share A rows
+  // in that XCD's L2; placement is a speed assumption only).
+  const int G = gridDim.x, x8 = blockIdx.x % 8, li = blockIdx.x / 8;
+  const int nbx = (G - x8 + 7) / 8;
+  const int cq = T / 8, cr = T % 8;
+  const int cbeg = x8 < cr ? x8 * (cq + 1) : cr * (cq + 1) + (x8 - cr) * cq;
+  const int cend = cbeg + cq + (x8 < cr ? 1 : 0);
+
+  const int64_t z = blockIdx.z;
+  const bf16_t* __restrict__ A = (const bf16_t*)args.A + z * args.strideA;
+  const bf16_t* __restrict__ B = (const bf16_t*)args.B + z * args.strideB;
+  const int64_t lda = args.lda, ldb = args.ldb;
+
+  const int S = SPLIT ? args.splitk : 1;
+  const int klen = ((K + S - 1) / S + 63) / 64 * 64;
+  const int kbeg = blockIdx.y * klen;
+  const int kend = min(K, kbeg + klen);
+  const int nt = kend > kbeg ? (kend - kbeg) / 64 : 0;
+
+  // per-lane DMA offsets, invariant over tiles and K-tiles
+  int voA[2][2], voB[2][2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      voA[sub][i] = half_voffset<LA, true>(lda, sub, i, wave, lane);
+      voB[sub][i] = half_voffset<LB, false>(ldb, sub, i, wave, lane);
+    }
+  // K-tile advance in bytes: along the row (KC) or down the k-rows (RC)
+  const int kstepA = LA == LAY_KC ? 2 : (int)(lda * 2), kstepB = LB == LAY_KC ? 2 : (int)(ldb * 2);
+  auto rsrcA = [&](int m0) {
+    return LA == LAY_KC ? make_rsrc(A + (int64_t)m0 * lda, ((int64_t)M - m0) * lda * 2)
+                        : make_rsrc(A + m0, ((int64_t)K * lda - m0) * 2);
+  };
+  auto rsrcB = [&](int n0) {
+    return LB == LAY_KC ? make_rsrc(B + (int64_t)n0 * ldb, ((int64_t)N - n0) * ldb * 2)
+                        : make_rsrc(B + n0, ((int64_t)K * ldb - n0) * 2);
+  };
+  // half h of K-tile t of the tile at (m0, n0): 0 = Am0, 1 = Am1, 2 = Bn0, 3 = Bn1
+  auto issue = [&](int m0, int n0, int t, int h) {
+    char* dst = smem + (t & 1) * BUF + h * HALF;
+    const int k0 = kbeg + t * 64;
+    if (h < 2) issue_half(rsrcA(m0), voA[h][0], voA[h][1], k0 * kstepA, dst, wave);
+    else issue_half(rsrcB(n0), voB[h - 2][0], voB[h - 2][1], k0 * kstepB, dst, wave);
+  };
+  // K-tile 0 whole + three halves of K-tile 1 (its Am1 follows in p0)
+  auto prologue = [&](int m0, int n0) {
+    issue(m0, n0, 0, 0);
+    issue(m0, n0, 0, 2);
+    issue(m0, n0, 0, 3);
+    issue(m0, n0, 0, 1);
+    if (nt > 1) {
+      issue(m0, n0, 1, 0);
+      issue(m0, n0, 1, 2);
+      issue(m0, n0, 1, 3);
+    }
+  };
+
+  bool primed = false, first = true, prev_full = false;
+#ifdef GEMM4_STAMPS
+  // diagnostic build only: s_memtime at tile start / after the DMA wait /
+  // after the K-loop / after the epilogue, waves 0 and 4 of every block
+  int ntile = 0;
+  const bool stamp = blockIdx.y == 0 && blockIdx.z == 0 && (wave == 0 || wave == 4) && lane == 0 && blockIdx.x < 256;
+  uint64_t* sp = g_stamps + ((int64_t)blockIdx.x * 8 * 2 + (wave >> 2)) * 4;
+#define STAMP(k) do { if (stamp && ntile < 8) sp[ntile * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+  for (int tile = cbeg + li; tile < cend; tile += nbx) {
+    STAMP(0);
+    const int bm = tile / gn, bn = tile % gn;
+    const int m0 = bm * 256, n0 = bn * 256;
+    const int tnext = tile + nbx;
+    const int m0n = (tnext / gn) * 256, n0n = (tnext % gn) * 256;
+    if (nt > 0 && !primed) prologue(m0, n0);
+    if (first && nt > 1) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (prev_full) {
+      // This tile's DMA was issued before the previous tile's epilogue, whose
+      // C stores (at least NST per wave for a full tile: 8 row fragments x 2
+      // x 16-B, twice that for fp32) are the youngest vector-memory ops: wait
+      // for everything older and let the stores drain behind this tile's
+      // MFMAs instead of stalling every CU on HBM writes at once.
+      if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    first = false;
+    prev_full = !SPLIT && m0 + 256 <= M && n0 + 256 <= N;
+    primed = false;
+    SEG_BARRIER();
+    if (wm == 1) SEG_BARRIER();
+    STAMP(1);
+
+    v4f acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+    v8s fa[4][2], fb[2][2][2];
+    for (int t = 0; t < nt; ++t) {
+      const char* buf = smem + (t & 1) * BUF;
+      const char* hA0 = buf;
+      const char* hA1 = buf + HALF;
+      const char* hB0 = buf + 2 * HALF;
+      const char* hB1 = buf + 3 * HALF;
+      const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+      // ---- p0: quadrant (0,0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = frag<LB>(hB0, 32 * wn + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA0, 64 * wm + 16 * i, ks, lane);
+      if (more1) issue(m0, n0, t + 1, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SEG_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      SEG_BARRIER();
+      // ---- p1: quadrant (0,1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = frag<LB>(hB1, 32 * wn + 16 * j, ks, lane);
+      if (more2) issue(m0, n0, t + 2, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SEG_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j][ks], fa[i][ks], acc[i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      SEG_BARRIER();
+      // ---- p2: quadrant (1,1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, 64 * wm + 16 * i, ks, lane);
+      if (more2) issue(m0, n0, t + 2, 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SEG_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 + i][2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j][ks], fa[i][ks], acc[4 + i][2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      SEG_BARRIER();
+      // ---- p3: quadrant (1,0), operands already in VGPRs. Every LDS read of
+      // this tile has been retired behind an earlier barrier, so the last
+      // K-tile starts the next output tile's DMA here.
+      if (more2) {
+        issue(m0, n0, t + 2, 3);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!more1 && tnext < cend) {
+          prologue(m0n, n0n);
+          primed = true;
+        }
+      }
+      SEG_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0 || more1) SEG_BARRIER();   // group 1 skips its very last one (it took one extra up front)
+    }
+    if (nt == 0 && wm == 0) SEG_BARRIER();
+    STAMP(2);
+    if (SPLIT) epilogue4_slab(args, acc, z, m0, n0, wm, wn, lane);
+    else epilogue4<OutT, EPI>(args, acc, z, m0, n0, wm, wn, lane);
+    STAMP(3);
+#ifdef GEMM4_STAMPS
+    ++ntile;
+#endif
+  }
+}
+
+template <int LA, int LB, typename OutT, int EPI>
+int launch4(const maeclip_gemm_args& a, hipStream_t s) {
+  const int gm = (int)((a.M + 255) / 256), gn = (int)((a.N + 255) / 256);
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  auto kern = S > 1 ? gemm4_kernel<LA, LB, OutT, EPI, true> : gemm4_kernel<LA, LB, OutT, EPI, false>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  // one block per CU (128 KiB LDS): persistent over tiles for plain launches;
+  // split-K / batched launches get one block per (tile, slice, batch)
+  const int tiles = gm * gn;
+  const int grid = (S * a.batch > 1 || tiles < ncu) ? tiles : ncu;
+  hipLaunchKernelGGL(kern, dim3(grid, S, (unsigned)a.batch), dim3(512), LDS_BYTES, s, a);
+  MC_CHECK_LAUNCH("maeclip_gemm(v4)");
+  return 0;
+}
+
+template <int LA, int LB, typename OutT>
+int epi4(const maeclip_gemm_args& a, hipStream_t s) {
+  switch (a.epilogue) {
+    case EPI_NONE: return launch4<LA, LB, OutT, EPI_NONE>(a, s);
+    case EPI_GELU: return launch4<LA, LB, OutT, EPI_GELU>(a, s);
+    case EPI_RESID: return launch4<LA, LB, OutT, EPI_RESID>(a, s);
+    case EPI_GELU_D: return launch4<LA, LB, OutT, EPI_GELU_D>(a, s);
+    case EPI_MUL_AUX: return launch4<LA, LB, OutT, EPI_MUL_AUX>(a, s);
+    default: return launch4<LA, LB, OutT, EPI_DGELU>(a, s);
+  }
+}
+
+template <int LA, int LB>
+int out4(const maeclip_gemm_args& a, hipStream_t s) {
+  return a.out_dtype == MAECLIP_BF16 ? epi4<LA, LB, bf16_t>(a, s) : epi4<LA, LB, float>(a, s);
+}
+
+}  // namespace
+
+#ifdef GEMM4_STAMPS
+extern "C" int maeclip_debug_gemm4_stamps(uint64_t* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(uint64_t) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
+
+namespace maeclip {
+// Shapes the v4 epilogue supports: 8 consecutive output columns per lane with
+// 16-B accesses on C / aux / resid.
+bool gemm_v4_ok(const maeclip_gemm_args& a) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (a.dtype != MAECLIP_BF16 || a.K % 64 != 0 || a.K <= 0 || a.lda % 8 || a.ldb % 8) return false;
+  if (a.M < 256 || a.N < 256 || a.N % 8) return false;
+  // buffer-descriptor DMA: every operand byte offset must fit 31 bits
+  const int64_t lim = 0x7fffffffLL;
+  if ((a.a_layout == LAY_KC ? a.M * a.lda : a.K * a.lda) * 2 >= lim) return false;
+  if ((a.b_layout == LAY_KC ? a.N * a.ldb : a.K * a.ldb) * 2 >= lim) return false;
+  if (a.splitk > 1) return al16(a.workspace);
+  if (!al16(a.C) || (a.out_dtype == MAECLIP_BF16 ? a.ldc % 8 : a.ldc % 4)) return false;
+  const bool wa = a.epilogue == EPI_GELU || a.epilogue == EPI_GELU_D;
+  const bool ra = a.epilogue == EPI_DGELU || a.epilogue == EPI_MUL_AUX;
+  if ((wa && a.aux_out && (!al16(a.aux_out) || a.ldaux % 8)) || (ra && (!al16(a.aux) || a.ldaux % 8))) return false;
+  if (a.resid && (!al16(a.resid) || a.ldr % 4)) return false;
+  if (a.bias && !al16(a.bias)) return false;
+  return true;
+}
+
+int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
+  if (a.a_layout == LAY_KC && a.b_layout == LAY_KC) return out4<LAY_KC, LAY_KC>(a, s);
+  if (a.a_layout == LAY_KC && a.b_layout == LAY_RC) return out4<LAY_KC, LAY_RC>(a, s);
+  if (a.a_layout == LAY_RC && a.b_layout == LAY_KC) return out4<LAY_RC, LAY_KC>(a, s);
+  return out4<LAY_RC, LAY_RC>(a, s);
+}
+}  // namespace maeclip

@@ -62,10 +62,11 @@ class TransformerStackFn(torch.autograd.Function):
             o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
             x1 = K.linear_fwd(o, wproj, bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
             h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T)
-            pre = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
-            a = K.linear_fwd(h2, w1, b1, epilogue=K.EPI_GELU, aux_out=pre)
+            # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
+            dgelu = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
+            a = K.linear_fwd(h2, w1, b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
             x2 = K.linear_fwd(a, w2, b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
-            saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, pre, a])
+            saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a])
             xi = x2
         ctx.saved = saved
         ctx.spec = spec
@@ -95,14 +96,14 @@ class TransformerStackFn(torch.autograd.Function):
             wqkv, wproj, w1, w2 = spec.wT[i]
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n2w = p[0], p[6]
-            xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, pre, a = ctx.saved[i]
+            xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
             gi = [None] * PER_BLOCK
-            # mlp.fc2 (+ GELU backward fused into the dgrad epilogue)
+            # mlp.fc2 (+ GELU backward fused into the dgrad epilogue: dA = (dy W2) * gelu'(h))
             gi[11] = rb.add(cpart)
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
-            dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_DGELU, aux=pre, colsum=dA_part)
+            dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
             gi[10] = K.linear_wgrad(gT, a)
-            del a, pre
+            del a, dgelu
             # mlp.fc1
             gi[9] = rb.add(dA_part)
             dh2 = K.linear_dgrad(dA, w1)

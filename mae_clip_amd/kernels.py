@@ -13,7 +13,7 @@ import torch
 from . import _lib as L
 
 KC, RC = 0, 1
-EPI_NONE, EPI_GELU, EPI_RESID, EPI_DGELU = 0, 1, 2, 3
+EPI_NONE, EPI_GELU, EPI_RESID, EPI_DGELU, EPI_GELU_D, EPI_MUL_AUX = 0, 1, 2, 3, 4, 5
 
 # Optional instrumentation: LAUNCH_HOOK(key, flops, launch_fn) wraps every GEMM
 # launch (bench.py brackets them with HIP events on the current stream).

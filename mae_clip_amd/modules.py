@@ -354,8 +354,7 @@ class DistilBertModel(nn.Module):
             a, _, _, aT, _ = K.ln_fwd(sa, lyr.sa_layer_norm.weight, lyr.sa_layer_norm.bias, 1e-12,
                                       out_dtype=torch.float32, res=h, want_stats=False, y2=bf)
             aT = aT if bf else a
-            pre = torch.empty((B * T, w1.shape[0]), device=x.device, dtype=dtype)
-            f1 = K.linear_fwd(aT, w1, lyr.ffn.lin1.bias, epilogue=K.EPI_GELU, aux_out=pre)
+            f1 = K.linear_fwd(aT, w1, lyr.ffn.lin1.bias, epilogue=K.EPI_GELU)   # frozen tower: no aux
             f2 = K.linear_fwd(f1, w2, lyr.ffn.lin2.bias, out_dtype=torch.float32)
             h, _, _, hT, _ = K.ln_fwd(f2, lyr.output_layer_norm.weight, lyr.output_layer_norm.bias, 1e-12,
                                       out_dtype=torch.float32, res=a, in_dropout=pdrop, seed_in=seed * 131 + 7 * li + 3,

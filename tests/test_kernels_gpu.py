@@ -21,7 +21,7 @@ def _ref_mm(A, B):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("lay", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("mnk", [(256, 256, 128), (200, 136, 72), (16, 8, 64), (384, 640, 1024)])
+@pytest.mark.parametrize("mnk", [(256, 256, 128), (200, 136, 72), (16, 8, 64), (384, 640, 1024), (264, 520, 64), (520, 264, 192)])
 def test_gemm_layouts(dev, dtype, lay, mnk):
     M, N, Kd = mnk
     a_lay, b_lay = lay
@@ -67,6 +67,18 @@ def test_gemm_epilogues(dev, dtype):
     g = torch.autograd.grad(torch.nn.functional.gelu(a64).sum(), a64)[0]
     ref_dx = _ref_mm(dy, w) * g
     assert (dx.double() - ref_dx).abs().max().item() < tol * 4
+    # GELU' epilogue (aux_out <- gelu'(pre)) and mul-aux: the MLP's fused pair
+    d = torch.empty((M, N), device=dev, dtype=dtype)
+    y4 = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU_D, aux_out=d)
+    r64 = ref.clone().requires_grad_(True)
+    gref = torch.autograd.grad(torch.nn.functional.gelu(r64).sum(), r64)[0]
+    assert (y4.double() - torch.nn.functional.gelu(ref)).abs().max().item() < tol * 4
+    assert (d.double() - gref).abs().max().item() < tol * 4
+    y5 = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU)   # no aux_out: gelu only
+    assert (y5.double() - torch.nn.functional.gelu(ref)).abs().max().item() < tol * 4
+    dx5 = K.linear_dgrad(dy, w, epilogue=K.EPI_MUL_AUX, aux=aux, out_dtype=torch.float32, resid=resid[:, :Kd].contiguous())
+    ref5 = _ref_mm(dy, w) * aux.double() + resid[:, :Kd].double()
+    assert (dx5.double() - ref5).abs().max().item() < tol * 4 * max(1.0, ref5.abs().max().item() / 4)
     # wgrad
     dW = K.linear_wgrad(dy, x)
     assert (dW.double() - _ref_mm(dy.t(), x)).abs().max().item() / _ref_mm(dy.t(), x).abs().max().item() < 1e-4

@@ -17,6 +17,12 @@ SHAPES = [  # (name, M, N, K, a_layout, b_layout)
     ("dec fc1 wgrad", 2048, 512, D, 1, 1), ("dec fc2 wgrad", 512, 2048, D, 1, 1), ("dec qkv wgrad", 1536, 512, D, 1, 1),
 ]
 
+if os.environ.get("GEMM_SET") == "sq":   # the guide's reference shapes + K sweep at fixed M, N
+    SHAPES = [("sq4096", 4096, 4096, 4096, 0, 0), ("sq8192", 8192, 8192, 8192, 0, 0),
+              ("4096x4096 K768", 4096, 4096, 768, 0, 0), ("4096x4096 K1536", 4096, 4096, 1536, 0, 0),
+              ("12800x3072 K768", E, 3072, 768, 0, 0), ("12800x3072 K3072", E, 3072, 3072, 0, 0),
+              ("sq4096 RC", 4096, 4096, 4096, 0, 1)]
+
 
 def mk(rows, cols):
     return (torch.randn(rows, cols, device=dev) * 0.5).to(torch.bfloat16)
