@@ -49,16 +49,101 @@ template <typename T, int HD> struct Img {
   static constexpr int CPR = BF ? HD / 8 : HD / 4;  // 16-B chunks per row
 };
 
-// global [n rows, stride ld] (head slice) -> LDS image, zero rows >= n up to npad
-template <typename T, int HD>
-__device__ __forceinline__ void load_img(char* lds, const T* __restrict__ g, int64_t ld, int n, int npad) {
+// NI head slices of the same token rows (global [n rows, stride ld]) -> NI
+// LDS images, zero rows >= n up to npad. Every thread keeps 2*NI 16-B loads in
+// flight before it writes LDS (the loop is latency-, not bandwidth-bound).
+template <typename T, int HD, int NI>
+__device__ __forceinline__ void load_imgs(char* const (&lds)[NI], const T* const (&g)[NI], int64_t ld, int n,
+                                          int npad) {
   using I = Img<T, HD>;
   const int total = npad * I::CPR;
-  for (int id = threadIdx.x; id < total; id += NTH) {
-    const int row = id / I::CPR, c = id % I::CPR;
-    v4u v = {0, 0, 0, 0};
-    if (row < n) v = *(const v4u*)(g + (int64_t)row * ld + c * (16 / sizeof(T)));
-    *(v4u*)(lds + I::chunk(row, c)) = v;
+  for (int id0 = threadIdx.x; id0 < total; id0 += 2 * NTH) {
+    v4u v[2][NI];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int id = id0 + u * NTH;
+      const int row = id / I::CPR, c = id % I::CPR;
+      const bool ok = id < total && row < n;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        v[u][i] = ok ? *(const v4u*)(g[i] + (int64_t)row * ld + c * (16 / sizeof(T))) : v4u{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int id = id0 + u * NTH;
+      const int row = id / I::CPR, c = id % I::CPR;
+      if (id < total) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) *(v4u*)(lds[i] + I::chunk(row, c)) = v[u][i];
+      }
+    }
+  }
+}
+
+// dot product of two 16-B chunks in f32
+template <typename T> __device__ __forceinline__ float chunk_dot(v4u a, v4u b);
+template <> __device__ __forceinline__ float chunk_dot<bf16_t>(v4u a, v4u b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s = fmaf(__uint_as_float(a[j] << 16), __uint_as_float(b[j] << 16), s);
+    s = fmaf(__uint_as_float(a[j] & 0xffff0000u), __uint_as_float(b[j] & 0xffff0000u), s);
+  }
+  return s;
+}
+template <> __device__ __forceinline__ float chunk_dot<float>(v4u a, v4u b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s = fmaf(__uint_as_float(a[j]), __uint_as_float(b[j]), s);
+  return s;
+}
+
+// Backward prologue: Q, K, V, dO images + Dv[q] = -rowsum(dO * O) (f32) +
+// L2[q] = -lse / c (-1e30 on padding rows), all rows in one pass with every load of an iteration in flight.
+// A row's CPR chunks sit on CPR consecutive lanes of one wave (CPR | 64, NTH a
+// multiple of 64, total a multiple of 64), so the row sum is an xor-shuffle.
+template <typename T, int HD>
+__device__ __forceinline__ void bwd_prologue(char* Qi, char* Ki, char* Vi, char* Di, float* L2, float* Dv,
+                                             const T* q, const T* k, const T* v, int64_t ld_qkv, const T* O,
+                                             const T* dO, int64_t ld_o, const float* lse, float inv_c, int n,
+                                             int npad) {
+  using I = Img<T, HD>;
+  constexpr int CPR = I::CPR, EPC = 16 / (int)sizeof(T);
+  const int total = npad * CPR;
+  for (int id0 = threadIdx.x; id0 < total; id0 += 2 * NTH) {
+    v4u vq[2], vk[2], vv[2], vd[2], vo[2];
+    float ls[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int id = id0 + u * NTH;
+      const int row = id / CPR, c = id % CPR;
+      const bool ok = id < total && row < n;
+      const int64_t oq = (int64_t)row * ld_qkv + c * EPC, oo = (int64_t)row * ld_o + c * EPC;
+      const v4u z = {0, 0, 0, 0};
+      vq[u] = ok ? *(const v4u*)(q + oq) : z;
+      vk[u] = ok ? *(const v4u*)(k + oq) : z;
+      vv[u] = ok ? *(const v4u*)(v + oq) : z;
+      vd[u] = ok ? *(const v4u*)(dO + oo) : z;
+      vo[u] = ok ? *(const v4u*)(O + oo) : z;
+      ls[u] = (ok && c == 0) ? -lse[row] * inv_c : -1.0e30f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int id = id0 + u * NTH;
+      if (id >= total) break;  // wave-uniform
+      const int row = id / CPR, c = id % CPR;
+      *(v4u*)(Qi + I::chunk(row, c)) = vq[u];
+      *(v4u*)(Ki + I::chunk(row, c)) = vk[u];
+      *(v4u*)(Vi + I::chunk(row, c)) = vv[u];
+      *(v4u*)(Di + I::chunk(row, c)) = vd[u];
+      float d = chunk_dot<T>(vd[u], vo[u]);
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) d += __shfl_xor(d, o, 64);
+      if (c == 0) {
+        Dv[row] = -d;
+        L2[row] = ls[u];
+      }
+    }
   }
 }
 
@@ -170,8 +255,11 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
 
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
   const int HH = H * HD;
-  load_img<T, HD>(Kimg, qkv + HH + h * HD, a.ld_qkv, n, npad);
-  load_img<T, HD>(Vimg, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
+  {
+    char* const dst[2] = {Kimg, Vimg};
+    const T* const src[2] = {qkv + HH + h * HD, qkv + 2 * HH + h * HD};
+    load_imgs<T, HD, 2>(dst, src, a.ld_qkv, n, npad);
+  }
   for (int k = threadIdx.x; k < npad; k += NTH) {
     float mk = (k < n) ? 0.f : NEG_BIG;
     if (k < n && a.key_mask && a.key_mask[(int64_t)b * n + k] == 0.f) mk = NEG_BIG;
@@ -211,25 +299,31 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
         }
       }
       float mloc = NEG_BIG;
+      if (kc + 64 > n || a.key_mask) {  // wave-uniform: padding / key-mask chunk
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) s[t][i] = fmaf(s[t][i], c, km[i]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) s[t] *= c;
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kc + 16 * t + 4 * g + i;
-          const float x = s[t][i] * c + kmask[key];
-          s[t][i] = x;
-          mloc = fmaxf(mloc, x);
-        }
+        for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
       mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float mnew = fmaxf(m, mloc);
-      const float alpha = exp2f(m - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float lp = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(s[t][i] - mnew);
+          const float p = __builtin_amdgcn_exp2f(s[t][i] - mnew);
           lp += p;
           s[t][i] = p;
         }
@@ -286,22 +380,8 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
   const T* O = (const T*)a.o + (int64_t)b * n * a.ld_o + h * HD;
   const T* dO = (const T*)a.dout + (int64_t)b * n * a.ld_o + h * HD;
-  load_img<T, HD>(Qi, qkv + h * HD, a.ld_qkv, n, npad);
-  load_img<T, HD>(Ki, qkv + HH + h * HD, a.ld_qkv, n, npad);
-  load_img<T, HD>(Vi, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
-  load_img<T, HD>(Di, dO, a.ld_o, n, npad);
-  // Dv[q] = rowsum(dO * O); one wave per row, fp32
-  for (int q = wave; q < npad; q += NW) {
-    float acc = 0.f;
-    if (q < n)
-      for (int d = lane; d < HD; d += 64)
-        acc += ld_as_f<T>(O + (int64_t)q * a.ld_o + d) * ld_as_f<T>(dO + (int64_t)q * a.ld_o + d);
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      Dv[q] = acc;
-      L2[q] = q < n ? a.lse[((int64_t)b * H + h) * n + q] : 3.0e38f;
-    }
-  }
+  bwd_prologue<T, HD>(Qi, Ki, Vi, Di, L2, Dv, qkv + h * HD, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv, O, dO,
+                      a.ld_o, a.lse + ((int64_t)b * H + h) * n, 1.f / (a.scale * LOG2E), n, npad);
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) cs[i] = 0.f;
   __syncthreads();
 
@@ -329,7 +409,8 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int q0 = qc + 16 * u;
-        v4f s = {0, 0, 0, 0}, dp = {0, 0, 0, 0};
+        // row constants as the initial accumulators: s' = S - lse/c, dp' = dP - Dv
+        v4f s = *(const v4f*)(L2 + q0 + 4 * g), dp = *(const v4f*)(Dv + q0 + 4 * g);
 #pragma unroll
         for (int ks = 0; ks < HD / 32; ++ks) {
           RowFrag<T, HD> qf, df;
@@ -338,12 +419,13 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
           s = mma32(qf, kf[ks], s);    // S[q=4g+i][key=lane&15]
           dp = mma32(df, vf[ks], dp);  // dP[q][key]
         }
+        // padding keys (lane >= n) only pollute their own dK/dV columns, which
+        // are never stored; padding queries have p = 0 (L2 = -1e30)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int qq = q0 + 4 * g + i;
-          const float p = kok ? exp2f(s[i] * c - L2[qq]) : 0.f;
+          const float p = __builtin_amdgcn_exp2f(s[i] * c);
           P[u][i] = p;
-          dS[u][i] = p * (dp[i] - Dv[qq]);
+          dS[u][i] = p * dp[i];
         }
       }
 #pragma unroll
@@ -400,7 +482,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int kb = kc + 16 * u;
-        v4f s = {0, 0, 0, 0}, dp = {0, 0, 0, 0};
+        v4f s = {lq, lq, lq, lq}, dp = {dq_, dq_, dq_, dq_};
 #pragma unroll
         for (int ks = 0; ks < HD / 32; ++ks) {
           RowFrag<T, HD> kf, vf;
@@ -410,10 +492,12 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
           dp = mma32(vf, df[ks], dp);  // dP^T
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kk = kb + 4 * g + i;
-          const float p = (kk < n) ? exp2f(s[i] * c - lq) : 0.f;
-          dST[u][i] = p * (dp[i] - dq_);
+        for (int i = 0; i < 4; ++i) dST[u][i] = __builtin_amdgcn_exp2f(s[i] * c) * dp[i];
+        // padding keys (last chunk only): K rows are zero, but an overflowing
+        // exp2(-lse) would turn 0 * inf into NaN in dQ, so zero them explicitly
+        if (kb + 16 > n) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dST[u][i] = (kb + 4 * g + i < n) ? dST[u][i] : 0.f;
         }
       }
 #pragma unroll
