@@ -343,6 +343,19 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const maeclip_gemm_a
   st4<OutT>(cp, v);
 }
 
+template <typename OutT>
+int splitk_reduce_t(const maeclip_gemm_args& a, hipStream_t s) {
+  const int64_t MN = a.M * a.N;
+  dim3 g2((unsigned)((MN / 4 + 255) / 256), (unsigned)a.batch);
+  hipLaunchKernelGGL((splitk_reduce_kernel<OutT>), g2, dim3(256), 0, s, a);
+  MC_CHECK_LAUNCH("maeclip_gemm(splitk reduce)");
+  return 0;
+}
+
+int splitk_reduce(const maeclip_gemm_args& a, hipStream_t s) {
+  return a.out_dtype == MAECLIP_BF16 ? splitk_reduce_t<bf16_t>(a, s) : splitk_reduce_t<float>(a, s);
+}
+
 template <typename T, typename OutT, int LA, int LB, int EPI>
 int launch(const maeclip_gemm_args& a, hipStream_t s) {
   const int gm = (int)((a.M + BM - 1) / BM), gn = (int)((a.N + BN - 1) / BN);
@@ -350,12 +363,7 @@ int launch(const maeclip_gemm_args& a, hipStream_t s) {
   dim3 grid(gm * gn, S, (unsigned)a.batch);
   hipLaunchKernelGGL((gemm_kernel<T, OutT, LA, LB, EPI>), grid, dim3(NT), 4 * TILE_BYTES, s, a);
   MC_CHECK_LAUNCH("maeclip_gemm");
-  if (S > 1) {
-    const int64_t MN = a.M * a.N;
-    dim3 g2((unsigned)((MN / 4 + 255) / 256), (unsigned)a.batch);
-    hipLaunchKernelGGL((splitk_reduce_kernel<OutT>), g2, dim3(256), 0, s, a);
-    MC_CHECK_LAUNCH("maeclip_gemm(splitk reduce)");
-  }
+  if (S > 1) return splitk_reduce_t<OutT>(a, s);
   return 0;
 }
 
@@ -412,15 +420,20 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
+  // v3/v4/v2 write raw fp32 split-K slabs and leave the reduction to
+  // splitk_reduce (v1's launch() reduces by itself)
+  int rc = 1;
   if (a->dtype == MAECLIP_BF16 && forced == 5 && a->epilogue <= EPI_DGELU && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
       a->M >= 256 && a->N >= 256)
-    return maeclip::gemm_v3(*a, s);
+    rc = maeclip::gemm_v3(*a, s);
   // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
   // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
-  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a)) return maeclip::gemm_v4(*a, s);
-  if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
-      (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
-    return maeclip::gemm_v2(*a, s, (forced == 5 || forced == 8) ? 0 : forced);
+  else if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
+    rc = maeclip::gemm_v4(*a, s);
+  else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+           (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
+    rc = maeclip::gemm_v2(*a, s, (forced == 5 || forced == 8) ? 0 : forced);
+  if (rc != 1) return (rc == 0 && a->splitk > 1) ? splitk_reduce(*a, s) : rc;
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);
   return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<float, bf16_t>(*a, s) : dispatch_lay<float, float>(*a, s);
@@ -428,14 +441,23 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
 
-// Slice count for split-K: aim for ~1024 workgroups (4 waves of 256 CUs at 2
-// blocks/CU... the wgrad shapes of the hot path have only 16-144 output tiles
-// but 12.8k-50k deep K), keeping >= 16 K-tiles of 64 per slice.
+// Slice count for split-K (the wgrad shapes of the hot path have only 4-36
+// output tiles of 256x256 but 12.8k-50k deep K). For shapes the v4 kernel takes
+// (one 128-KiB-LDS block per CU) fill the 256 CUs exactly once: S = 256/tiles,
+// at least 8 K-tiles of 64 per slice -- every extra slice costs an fp32 slab
+// write + read in splitk_reduce. Other shapes (v1 128x128 tiles, several blocks
+// per CU): ~1024 workgroups, >= 16 K-tiles per slice.
 extern "C" int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int64_t s = 1024 / (tiles > 0 ? tiles : 1);
-  const int64_t kmax = K / 1024;
-  if (s > kmax) s = kmax;
+  int64_t s;
+  if (M >= 256 && N >= 256 && K % 64 == 0) {
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    s = 256 / tiles;
+    if (s > K / 512) s = K / 512;
+  } else {
+    const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    s = 1024 / (tiles > 0 ? tiles : 1);
+    if (s > K / 1024) s = K / 1024;
+  }
   if (s > 64) s = 64;
   return (int32_t)(s < 1 ? 1 : s);
 }

@@ -200,6 +200,22 @@ def test_wgrad_splitk(dev, dtype):
     assert torch.equal(dW, dW2)  # deterministic
 
 
+@pytest.mark.parametrize("mnk", [(12800, 768, 768), (4096, 512, 2048), (3200, 2304, 768)])
+def test_wgrad_splitk_v4(dev, mnk):
+    """Production wgrad shapes (bf16, token dim % 64 == 0, >= 256x256 output):
+    the v4 kernel's split-K slabs + deterministic splitk_reduce."""
+    M, N, Kd = mnk
+    from mae_clip_amd import _lib
+    assert _lib.lib().maeclip_gemm_splitk(N, Kd, M) > 1
+    dy = _rand((M, N), torch.bfloat16, dev, seed=44)
+    x = _rand((M, Kd), torch.bfloat16, dev, seed=45)
+    dW = K.linear_wgrad(dy, x)
+    ref = _ref_mm(dy.t(), x)
+    assert (dW.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-5
+    dW2 = K.linear_wgrad(dy, x)
+    assert torch.equal(dW, dW2)
+
+
 def test_colsum_two_pass(dev):
     part = _rand((1000, 768), torch.float32, dev, seed=43)
     out = K.colsum_reduce(part)
