@@ -102,26 +102,74 @@ def cpu_baseline(seconds_budget=20.0):
 
 
 class KernelTimer:
-    """Brackets every GEMM launch with HIP events on the launching stream during
-    the timed steps; reports the (shape) with the largest total time."""
+    """Brackets GEMM launches with HIP events on the launching stream; reports
+    the shape with the largest total time.
+
+    Eager steps: one HIP event pair per launch. Under HIP-graph capture
+    torch-ROCm refuses event-record nodes ("External events are disallowed in
+    rocm"), so the launch is bracketed by two 1-lane timestamp kernels on the
+    same stream (maeclip_timestamp: s_memrealtime, 100 MHz) that are captured
+    with it; every replay re-times it and harvest() collects the spans after
+    each timed step."""
 
     def __init__(self):
         self.records = {}
         self.active = False
+        self.only = None     # timed region: bracket only this key's launches
+        self.captured = []   # (key, flops, slot) bracketed inside the graph
+        self.ts = None       # device int64 [2 * slots] timestamps
 
     def hook(self, key, flops, launch):
-        if not self.active:
+        if not self.active or (self.only is not None and key != self.only):
             return launch()
+        from mae_clip_amd.functions import side_stream
+        if torch.cuda.current_stream() == side_stream(torch.device("cuda", torch.cuda.current_device())):
+            # side-stream launches (text tower, weight gradients) overlap the
+            # main chain by design: their event spans are not kernel durations
+            return launch()
+        if torch.cuda.is_current_stream_capturing():
+            from mae_clip_amd import _lib
+            lib, st = _lib.lib(), torch.cuda.current_stream().cuda_stream
+            if self.ts is None:
+                self.ts = torch.zeros(2 * 64, dtype=torch.int64, device="cuda")
+            i = len(self.captured)
+            if i >= 64:
+                return launch()
+            _lib.check(lib.maeclip_timestamp(self.ts.data_ptr() + 16 * i, st), "maeclip_timestamp")
+            launch()
+            _lib.check(lib.maeclip_timestamp(self.ts.data_ptr() + 16 * i + 8, st), "maeclip_timestamp")
+            self.captured.append((key, flops, i))
+            return
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
         self.records.setdefault(key, [flops, []])[1].append((s, e))
 
+    def harvest(self):
+        """After a synchronised replay: add the captured launches' durations (ms)."""
+        if not self.captured:
+            return
+        from mae_clip_amd import _lib
+        khz = float(_lib.lib().maeclip_wallclock_khz()) or 100000.0
+        t = self.ts.view(-1, 2).cpu()
+        for key, flops, i in self.captured:
+            self.records.setdefault(key, [flops, []])[1].append(float(t[i, 1] - t[i, 0]) / khz)
+
+    def table(self, steps, file):
+        rows = []
+        for key, (flops, evs) in self.records.items():
+            ms = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in evs]
+            rows.append((sum(ms) / steps, len(ms) / steps, flops / (sum(ms) / len(ms)) / 1e9, key))
+        rows.sort(reverse=True)
+        print(f"GEMM total {sum(r[0] for r in rows):.3f} ms/step", file=file)
+        for t, n, tf, key in rows:
+            print(f"{t:8.3f} ms/step {n:5.1f} launches/step {tf:7.1f} TF/s  {key}", file=file)
+
     def summary(self):
         best = None
         for key, (flops, evs) in self.records.items():
-            ms = [a.elapsed_time(b) for a, b in evs]
+            ms = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in evs]
             tot = sum(ms)
             if best is None or tot > best[2]:
                 best = (key, flops, tot, len(ms))
@@ -138,6 +186,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one HIP graph per step")
+    ap.add_argument("--gemm-table", action="store_true", help="per-shape GEMM times to stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,6 +201,7 @@ def main():
     from mae_clip_amd import kernels as K
     from mae_clip_amd.optim import AdamW
     from mae_clip_amd.distributed import DataParallel
+    from mae_clip_amd.graph import CapturedStep
 
     model = build_model(dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6,
                              mask_ratio=args.mask_ratio, decoder_embed_dim=512, decoder_depth=8,
@@ -164,19 +215,37 @@ def main():
     if not args.no_kernel_timer:
         K.LAUNCH_HOOK = timer.hook
 
+    # one HIP graph per step (mae_clip_amd.graph): step 1 eager, step 2 captured,
+    # then replays. Data-parallel runs and --gemm-table stay eager.
+    use_graph = world == 1 and not args.no_graph and not args.gemm_table
+    runner = CapturedStep(model, opt, enabled=use_graph, eager_steps=2)
+    warmup = max(args.warmup, 3) if use_graph else max(args.warmup, 2)
+
     def step():
+        if dp is None:
+            # after capture the graph's static input buffers ARE the batch
+            # (synthetic inputs resident in HBM): no per-step copy
+            return runner.step(runner.static if runner.static is not None else batch)
         opt.zero_grad(set_to_none=True)
         loss = model(batch)
         loss.backward()
-        if dp is not None:
-            dp.sync_gradients()
+        dp.sync_gradients()
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
+    # warm-up: time every GEMM launch of the second (eager, warm) step to find
+    # the dominant shape; afterwards only that shape's launches are bracketed
+    # (~8 per step instead of ~250; in graph mode the brackets are captured
+    # with the step at i == 2 and re-timed by every replay)
+    for i in range(warmup):
+        timer.active = (i == 1) or args.gemm_table or (use_graph and i == 2)
         loss = step()
         loss.item()
+        if i == 1 and timer.records and not args.gemm_table:
+            timer.only = timer.summary()[0]
+            timer.records = {}
     torch.cuda.synchronize()
+    timer.records = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -185,6 +254,7 @@ def main():
     for _ in range(args.steps):
         loss = step()
         loss.item()  # main.py:64 syncs every step
+        timer.harvest()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timer.active = False
@@ -197,6 +267,8 @@ def main():
     value = global_batch * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
 
+    if rank == 0 and args.gemm_table and not args.no_kernel_timer:
+        timer.table(args.steps, sys.stderr)
     if rank == 0:
         roof = None
         best = timer.summary() if not args.no_kernel_timer else None

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 1
+#define MAECLIP_ABI_VERSION 2
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -83,6 +83,9 @@ typedef struct {
 } maeclip_gemm_args;
 int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
 int64_t maeclip_gemm_colsum_rows(int64_t M);
+/* scratch bytes maeclip_gemm may use for *args when args->splitk <= 1 (pass
+ * them as args->workspace; a NULL workspace is always valid, just slower) */
+int64_t maeclip_gemm_workspace(const maeclip_gemm_args* args);
 int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K);
 
 /* ------------------------------------------------------------- attention
@@ -107,6 +110,9 @@ typedef struct {
   int32_t B, n, H, head_dim, dtype;
   float scale, dropout_p;
   uint64_t seed;
+  /* optional device step counter: dropout seed = seed + (*step_ptr) * MAECLIP_STEP_MULT
+   * (so a captured HIP graph draws fresh masks every replay) */
+  const int64_t* step_ptr;
 } maeclip_attn_args;
 int32_t maeclip_attn_fwd(const maeclip_attn_args* args, void* stream);
 int32_t maeclip_attn_bwd(const maeclip_attn_args* args, void* stream);
@@ -133,6 +139,7 @@ typedef struct {
   float* rstd;
   float out_dropout_p;
   uint64_t seed_in, seed_out;
+  const int64_t* step_ptr; /* optional: both seeds + (*step_ptr) * MAECLIP_STEP_MULT */
   int64_t M, D, ldx, ldy;
   float eps;
 } maeclip_ln_fwd_args;
@@ -188,7 +195,8 @@ int32_t maeclip_rows_colsum_partial_rows(int64_t M);
 int32_t maeclip_pool_fwd(const float* x, int32_t B, int32_t n, int32_t D, float* out, void* stream);
 int32_t maeclip_pool_bwd(const float* dout, int32_t B, int32_t n, int32_t D, float* dx, int32_t accumulate, void* stream);
 /* nn.Dropout with the library's counter-based mask (same as LN in_dropout) */
-int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed, void* stream);
+int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed,
+                        const int64_t* step_ptr, void* stream);
 /* DistilBERT Embeddings word+position gather (modeling_distilbert.py:92-117) */
 int32_t maeclip_embed_fwd(const int64_t* ids, const float* word, const float* pos, int32_t B, int32_t T, int32_t D,
                           int64_t V, float* out, void* stream);
@@ -208,6 +216,9 @@ typedef struct {
   float step_size; /* lr / (1 - beta1^t) */
   float bc2_sqrt;  /* sqrt(1 - beta2^t) */
   float grad_scale;
+  /* optional device step count t (>= 1): when set, step_size and bc2_sqrt are
+   * recomputed in the kernel from lr, beta1, beta2 and *step_ptr */
+  const int64_t* step_ptr;
 } maeclip_adamw_hparams;
 int64_t maeclip_mt_chunk(void);
 /* dev_entries: device copy of host_entries (host pointer used for the grid size) */
@@ -227,6 +238,7 @@ typedef struct {
   float* noise;
   int32_t B, L, len_keep;
   uint64_t seed, step, sample_offset;
+  const int64_t* step_ptr; /* optional: step used = step + *step_ptr */
 } maeclip_mask_args;
 int32_t maeclip_mask_ids(const maeclip_mask_args* args, void* stream);
 
@@ -322,6 +334,17 @@ typedef struct {
 } maeclip_clip_args;
 size_t maeclip_clip_loss_workspace(int64_t N);
 int32_t maeclip_clip_loss(const maeclip_clip_args* args, void* stream);
+
+/* ------------------------------------------------------------ step state
+ * Device-resident step counters (model RNG step, optimizer step t) so that a
+ * whole training step can be captured once in a HIP graph and replayed. */
+#define MAECLIP_STEP_MULT 0x9E3779B97F4A7C15ull
+int32_t maeclip_counter_add(int64_t* counter, int64_t delta, void* stream);
+/* stream-ordered device timestamp (REALTIME counter, maeclip_wallclock_khz ticks/ms) */
+int32_t maeclip_timestamp(int64_t* dst, void* stream);
+int64_t maeclip_wallclock_khz(void);
+/* stream-ordered host->device copy (pinned src), capturable into a HIP graph */
+int32_t maeclip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,11 @@ class CLIPModel(nn.Module):
         else:
             self.mae_decoder = None
         self.step = 0
+        # device-resident step: keys the MAE mask noise and every dropout mask, and
+        # is advanced by a kernel at the end of each training forward, so a
+        # captured HIP graph of the step (mae_clip_amd.graph) draws fresh masks
+        # on every replay. Not persistent: state_dict keys stay the reference's.
+        self.register_buffer("step_counter", torch.zeros(1, dtype=torch.int64), persistent=False)
         self.last_losses = {}
         self.process_group = None
         self._cache = None
@@ -74,11 +79,13 @@ class CLIPModel(nn.Module):
             return 1, 0
         return torch.distributed.get_world_size(pg), torch.distributed.get_rank(pg)
 
-    def masking(self, B, step, sample_offset, device):
+    def masking(self, B, sample_offset, device):
+        """HF random_masking ids of the current device step (step_counter)."""
         vit = self.image_encoder.model
         L = vit.patch_embed.num_patches
         keep = int(L * (1 - self.mask_ratio))
-        ids_shuffle, ids_restore, mask, _ = K.mask_ids(B, L, keep, self.mask_seed, step, sample_offset, device)
+        ids_shuffle, ids_restore, mask, _ = K.mask_ids(B, L, keep, self.mask_seed, 0, sample_offset, device,
+                                                       step_ptr=self.step_counter)
         return ids_shuffle, ids_restore, mask, keep
 
     def forward(self, batch):
@@ -86,16 +93,30 @@ class CLIPModel(nn.Module):
         if not img.is_cuda:
             raise RuntimeError("mae_clip_amd.CLIPModel needs the batch on a ROCm device (no CPU fallback)")
         dtype = compute_dtype(self.precision)
-        cache = self._weight_cache()
-        cache.refresh(dtype)
         vit = self.image_encoder.model
         B = img.shape[0]
         world, rank = self._world()
-        step = self.step
-        seed = (self.dropout_seed * 1000003 + step * 8191 + rank) & 0x7FFFFFFFFFFFFFFF
+        sc = self.step_counter
+        if not sc.is_cuda:
+            raise RuntimeError("CLIPModel.step_counter must live on the GPU (call .to(device))")
+        # step-independent seed base; the kernels add step_counter * MAECLIP_STEP_MULT
+        seed = (self.dropout_seed * 1000003 + rank) & 0x7FFFFFFFFFFFFFFF
+        # the frozen text tower (no autograd, own bf16 weights) is independent of
+        # the image path: it runs on the side stream, overlapped with the image
+        # encoder, and is issued first so it also overlaps the weight-shadow cast
+        use_side = bool(CFG.side_stream)
+        main = torch.cuda.current_stream(img.device)
+        if use_side:
+            side = Fn.side_stream(img.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17,
+                                                  dtype=dtype, step_ptr=sc)
+        cache = self._weight_cache()
+        cache.refresh(dtype)
         mae = self.mae_decoder is not None
         if mae:
-            ids_shuffle, ids_restore, mask, keep = self.masking(B, step, rank * B, img.device)
+            ids_shuffle, ids_restore, mask, keep = self.masking(B, rank * B, img.device)
             tokens = vit.forward_tokens(img, dtype, cache, ids_shuffle, ids_restore, keep)
             dec = self.mae_decoder
             feat, latent = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias,
@@ -103,9 +124,14 @@ class CLIPModel(nn.Module):
         else:
             tokens = vit.forward_tokens(img, dtype, cache)
             feat = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias, None, None)
-        text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17, dtype=dtype)
-        image_embeddings = self.image_projection(feat, seed=seed + 29)
-        text_embeddings = self.text_projection(text_features, seed=seed + 31)
+        if use_side:
+            main.wait_stream(side)
+            text_features.record_stream(main)
+        else:
+            text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17,
+                                              dtype=dtype, step_ptr=sc)
+        image_embeddings = self.image_projection(feat, seed=seed + 29, step_ptr=sc)
+        text_embeddings = self.text_projection(text_features, seed=seed + 31, step_ptr=sc)
         if world > 1:
             from .distributed import gather_rows
             image_embeddings = gather_rows(image_embeddings, self.process_group)
@@ -130,6 +156,7 @@ class CLIPModel(nn.Module):
             self.last_mask = (ids_shuffle, ids_restore, mask)
         if self.training:
             self.step += 1
+            K.counter_add(sc, 1)
         return loss
 
 

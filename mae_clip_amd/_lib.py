@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -35,14 +35,14 @@ class AttnArgs(C.Structure):
                 ("key_mask", c_vp), ("colsum_partial", c_vp),
                 ("ld_qkv", c_i64), ("ld_o", c_i64), ("ld_dqkv", c_i64),
                 ("B", c_i32), ("n", c_i32), ("H", c_i32), ("head_dim", c_i32), ("dtype", c_i32),
-                ("scale", c_f32), ("dropout_p", c_f32), ("seed", c_u64)]
+                ("scale", c_f32), ("dropout_p", c_f32), ("seed", c_u64), ("step_ptr", c_vp)]
 
 
 class LnFwdArgs(C.Structure):
     _fields_ = [("x", c_vp), ("x_dtype", c_i32), ("res", c_vp), ("ldres", c_i64), ("in_dropout_p", c_f32),
                 ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_i32), ("y2", c_vp), ("ldy2", c_i64),
                 ("xsum_out", c_vp), ("ldxs", c_i64), ("mean", c_vp), ("rstd", c_vp), ("out_dropout_p", c_f32),
-                ("seed_in", c_u64), ("seed_out", c_u64),
+                ("seed_in", c_u64), ("seed_out", c_u64), ("step_ptr", c_vp),
                 ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("ldy", c_i64), ("eps", c_f32)]
 
 
@@ -66,13 +66,13 @@ class ColsumEntry(C.Structure):
 
 class AdamwHparams(C.Structure):
     _fields_ = [("lr", c_f32), ("beta1", c_f32), ("beta2", c_f32), ("eps", c_f32), ("weight_decay", c_f32),
-                ("step_size", c_f32), ("bc2_sqrt", c_f32), ("grad_scale", c_f32)]
+                ("step_size", c_f32), ("bc2_sqrt", c_f32), ("grad_scale", c_f32), ("step_ptr", c_vp)]
 
 
 class MaskArgs(C.Structure):
     _fields_ = [("ids_shuffle", c_vp), ("ids_restore", c_vp), ("mask", c_vp), ("noise", c_vp),
                 ("B", c_i32), ("L", c_i32), ("len_keep", c_i32),
-                ("seed", c_u64), ("step", c_u64), ("sample_offset", c_u64)]
+                ("seed", c_u64), ("step", c_u64), ("sample_offset", c_u64), ("step_ptr", c_vp)]
 
 
 class PatchArgs(C.Structure):
@@ -114,6 +114,7 @@ _SIGS = {
     "maeclip_device_count": (c_i32, []),
     "maeclip_gemm": (c_i32, [C.POINTER(GemmArgs), c_vp]),
     "maeclip_gemm_colsum_rows": (c_i64, [c_i64]),
+    "maeclip_gemm_workspace": (c_i64, [C.POINTER(GemmArgs)]),
     "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
     "maeclip_attn_fwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_attn_bwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
@@ -125,7 +126,7 @@ _SIGS = {
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "maeclip_pool_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp]),
-    "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp]),
+    "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp, c_vp]),
     "maeclip_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp]),
     "maeclip_mt_chunk": (c_i64, []),
     "maeclip_colsum_multi": (c_i32, [c_vp, C.POINTER(ColsumEntry), c_i32, c_vp]),
@@ -141,6 +142,10 @@ _SIGS = {
     "maeclip_mae_loss_bwd": (c_i32, [C.POINTER(MaeLossArgs), c_vp]),
     "maeclip_clip_loss_workspace": (c_sz, [c_i64]),
     "maeclip_clip_loss": (c_i32, [C.POINTER(ClipArgs), c_vp]),
+    "maeclip_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
+    "maeclip_memcpy_h2d": (c_i32, [c_vp, c_vp, c_sz, c_vp]),
+    "maeclip_timestamp": (c_i32, [c_vp, c_vp]),
+    "maeclip_wallclock_khz": (c_i64, []),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -66,3 +66,5 @@ text_attention_dropout = 0.1
 precision = "bf16"         # "bf16" (perf) or "fp32" (parity mode, exact-f32 MFMA)
 mask_seed = 2
 dropout_seed = 1234
+# ---- scheduling
+side_stream = True         # frozen text tower || image encoder; weight-gradient GEMMs || the dgrad chain

@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int key = kc + 16 * t + 4 * g + i;
-            s[t][i] = dropout_keep(a.seed, bh, q, key, thr) ? s[t][i] * dscale : 0.f;
+            s[t][i] = dropout_keep(mc_step_seed(a.seed, a.step_ptr), bh, q, key, thr) ? s[t][i] * dscale : 0.f;
           }
       }
 #pragma unroll

@@ -151,6 +151,10 @@ __host__ __device__ __forceinline__ uint64_t mc_mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+// seed of a dropout / noise draw at the current device step (MAECLIP_STEP_MULT, maeclip.h)
+__device__ __forceinline__ uint64_t mc_step_seed(uint64_t seed, const int64_t* step_ptr) {
+  return step_ptr ? seed + (uint64_t)(*step_ptr) * 0x9E3779B97F4A7C15ull : seed;
+}
 __host__ __device__ __forceinline__ uint32_t mc_hash4(uint64_t seed, uint64_t a, uint64_t b, uint64_t c) {
   uint64_t h = mc_mix64(seed);
   h = mc_mix64(h ^ a);

@@ -89,13 +89,13 @@ __global__ void __launch_bounds__(NTH) pool_bwd_kernel(const float* __restrict__
 
 // y = x * keep/(1-p) with the same mask function as the LayerNorm input dropout
 __global__ void __launch_bounds__(NTH) dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t M, int D,
-                                                      int64_t ld, float p, uint64_t seed) {
+                                                      int64_t ld, float p, uint64_t seed, const int64_t* step_ptr) {
   const int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x;
   if (i >= M * D) return;
   const int64_t r = i / D;
   const int c = (int)(i % D);
   const uint32_t thr = (uint32_t)((double)p * 4294967296.0);
-  const float k = mc_hash4(seed, (uint64_t)r, (uint64_t)c, 0x4c4eull) >= thr ? 1.f / (1.f - p) : 0.f;
+  const float k = mc_hash4(mc_step_seed(seed, step_ptr), (uint64_t)r, (uint64_t)c, 0x4c4eull) >= thr ? 1.f / (1.f - p) : 0.f;
   y[r * ld + c] = x[r * ld + c] * k;
 }
 
@@ -232,13 +232,19 @@ __global__ void __launch_bounds__(NTH) adamw_multi_kernel(const maeclip_mt_entry
   const int64_t n = e[k].n;
   const float decay = 1.f - hp.lr * hp.weight_decay;
   const float b1 = hp.beta1, b2 = hp.beta2;
+  float step_size = hp.step_size, bc2_sqrt = hp.bc2_sqrt;
+  if (hp.step_ptr) {   // device step count t: bias corrections of torch's _single_tensor_adamw
+    const float t = (float)*hp.step_ptr;
+    step_size = hp.lr / (1.f - powf(b1, t));
+    bc2_sqrt = sqrtf(1.f - powf(b2, t));
+  }
   for (int64_t i = base + threadIdx.x; i < base + CHUNK && i < n; i += NTH) {
     const float g = gr[i] * hp.grad_scale;
     float pi = p[i] * decay;
     const float mi = b1 * m[i] + (1.f - b1) * g;
     const float vi = b2 * v[i] + (1.f - b2) * g * g;
-    const float denom = sqrtf(vi) / hp.bc2_sqrt + hp.eps;
-    pi -= hp.step_size * mi / denom;
+    const float denom = sqrtf(vi) / bc2_sqrt + hp.eps;
+    pi -= step_size * mi / denom;
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -322,12 +328,12 @@ extern "C" int32_t maeclip_pool_bwd(const float* dout, int32_t B, int32_t n, int
 }
 
 extern "C" int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed,
-                                   void* stream) {
+                                   const int64_t* step_ptr, void* stream) {
   MC_CHECK_ARG(x && y && M >= 0 && D > 0 && p >= 0.f && p < 1.f, "maeclip_dropout: bad args");
   if (M == 0) return 0;
   const int64_t total = M * D;
   hipLaunchKernelGGL(dropout_kernel, dim3((unsigned)((total + NTH - 1) / NTH)), dim3(NTH), 0, (hipStream_t)stream, x, y, M,
-                     D, ld, p, seed);
+                     D, ld, p, seed, step_ptr);
   MC_CHECK_LAUNCH("maeclip_dropout");
   return 0;
 }
@@ -358,5 +364,29 @@ extern "C" int32_t maeclip_adamw_multi(const maeclip_mt_entry* dev_entries, cons
   if (nb == 0) return 0;
   hipLaunchKernelGGL(adamw_multi_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, dev_entries, ne, *hp);
   MC_CHECK_LAUNCH("maeclip_adamw_multi");
+  return 0;
+}
+
+namespace {
+__global__ void counter_add_kernel(int64_t* c, int64_t delta) {
+  if (threadIdx.x == 0) *c += delta;
+}
+}  // namespace
+
+extern "C" int32_t maeclip_counter_add(int64_t* counter, int64_t delta, void* stream) {
+  MC_CHECK_ARG(counter != nullptr, "maeclip_counter_add: null counter");
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta);
+  MC_CHECK_LAUNCH("maeclip_counter_add");
+  return 0;
+}
+
+extern "C" int32_t maeclip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  MC_CHECK_ARG(dst && src, "maeclip_memcpy_h2d: null pointer");
+  if (bytes == 0) return 0;
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    maeclip::set_error("maeclip_memcpy_h2d: %s", hipGetErrorString(e));
+    return -2;
+  }
   return 0;
 }

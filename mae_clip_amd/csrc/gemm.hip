@@ -33,6 +33,9 @@ int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v3(const maeclip_gemm_args& a, hipStream_t s);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
+int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
+bool gemm_small_ok(const maeclip_gemm_args& a);
+int64_t gemm_small_workspace(const maeclip_gemm_args& a);
 }
 
 namespace {
@@ -422,6 +425,7 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
   // v3/v4/v2 write raw fp32 split-K slabs and leave the reduction to
   // splitk_reduce (v1's launch() reduces by itself)
+  if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small(*a, s);
   int rc = 1;
   if (a->dtype == MAECLIP_BF16 && forced == 5 && a->epilogue <= EPI_DGELU && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
       a->M >= 256 && a->N >= 256)
@@ -440,6 +444,14 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 }
 
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
+
+// Scratch bytes maeclip_gemm may use for this call when the caller asks for no
+// split-K itself (splitk <= 1): the small-fp32 path's K-slice partials.
+extern "C" int64_t maeclip_gemm_workspace(const maeclip_gemm_args* a) {
+  if (!a || a->splitk > 1) return 0;
+  static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
+  return (forced != 99 && maeclip::gemm_small_ok(*a)) ? maeclip::gemm_small_workspace(*a) : 0;
+}
 
 // Slice count for split-K (the wgrad shapes of the hot path have only 4-36
 // output tiles of 256x256 but 12.8k-50k deep K). For shapes the v4 kernel takes

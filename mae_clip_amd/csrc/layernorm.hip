@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[c][j] *= keepf(a.seed_in, row, c * 256 + lane * 4 + j, thr, sc);
+      for (int j = 0; j < 4; ++j) v[c][j] *= keepf(mc_step_seed(a.seed_in, a.step_ptr), row, c * 256 + lane * 4 + j, thr, sc);
   }
   if (a.res) {
     float r[NC][4];
@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       y[j] = (v[c][j] - mean) * rstd * gm[j] + bt[j];
-      if (odrop) y[j] *= keepf(a.seed_out, row, e + j, othr, osc);
+      if (odrop) y[j] *= keepf(mc_step_seed(a.seed_out, a.step_ptr), row, e + j, othr, osc);
     }
     st4<YT>((YT*)a.y + row * a.ldy + e, y);
     if (a.y2) st4<bf16_t>((bf16_t*)a.y2 + row * a.ldy2 + e, y);

@@ -28,9 +28,10 @@ __global__ void __launch_bounds__(NTH) mask_ids_kernel(const maeclip_mask_args a
   int S2 = 1;
   while (S2 < L) S2 <<= 1;
   const uint64_t gb = (uint64_t)a.sample_offset + b;
+  const uint64_t step = a.step + (a.step_ptr ? (uint64_t)*a.step_ptr : 0ull);
   for (int i = threadIdx.x; i < S2; i += NTH) {
     if (i < L) {
-      const uint64_t k24 = mc_hash4(a.seed, a.step, gb, (uint64_t)i) >> 8;
+      const uint64_t k24 = mc_hash4(a.seed, step, gb, (uint64_t)i) >> 8;
       keys[i] = (k24 << 10) | (uint64_t)i;
       if (a.noise) a.noise[(int64_t)b * L + i] = (float)k24 * (1.0f / 16777216.0f);
     } else {

@@ -20,3 +20,27 @@ extern "C" int32_t maeclip_device_count(void) {
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
 }
+
+// Stream-ordered device timestamp: one lane writes the 100-MHz constant
+// REALTIME counter (s_memrealtime, a scalar-cache READ) to *dst with a vector
+// store. Bracketing a launch with two of these times it inside a captured HIP
+// graph, where torch-ROCm refuses event-record nodes.
+namespace {
+__global__ void timestamp_kernel(int64_t* dst) {
+  if (threadIdx.x == 0) *dst = (int64_t)__builtin_amdgcn_s_memrealtime();
+}
+}  // namespace
+
+extern "C" int32_t maeclip_timestamp(int64_t* dst, void* stream) {
+  MC_CHECK_ARG(dst != nullptr, "maeclip_timestamp: null dst");
+  hipLaunchKernelGGL(timestamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst);
+  MC_CHECK_LAUNCH("maeclip_timestamp");
+  return 0;
+}
+
+extern "C" int64_t maeclip_wallclock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+  return khz;
+}

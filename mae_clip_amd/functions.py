@@ -29,6 +29,53 @@ def _reduce(part):
     return K.colsum_reduce(part)
 
 
+# ------------------------------------------------------------ side stream
+_SIDE = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """One extra HIP stream per device for work that is independent of the
+    current stream's chain (weight gradients, the frozen text tower)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+class WgradQueue:
+    """Weight-gradient GEMMs of a backward pass on the side stream.
+
+    Each dW = dy^T x only feeds the optimizer, so it runs beside the
+    dgrad -> LN -> attention chain of the current stream and fills the CUs that
+    chain leaves idle (the tails of its persistent GEMMs, the HBM-bound LN /
+    attention kernels). Inputs get record_stream() so the caching allocator
+    does not hand their memory to the current stream while the side stream may
+    still read it; join() makes the current stream wait for every queued dW.
+    """
+
+    def __init__(self, device, enabled=True):
+        self.main = torch.cuda.current_stream(device)
+        self.side = side_stream(device) if enabled else None
+
+    def wgrad(self, dy, x):
+        if self.side is None:
+            return K.linear_wgrad(dy, x)
+        M, N = dy.shape
+        out = torch.empty((N, x.shape[1]), device=dy.device, dtype=torch.float32)
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            K.linear_wgrad(dy, x, out=out)
+        dy.record_stream(self.side)
+        x.record_stream(self.side)
+        out.record_stream(self.side)
+        return out
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+
+
 # ---------------------------------------------------------------- stacks
 @dataclass
 class StackSpec:
@@ -39,6 +86,7 @@ class StackSpec:
     eps: float
     dtype: torch.dtype              # compute dtype of GEMM operands / activations
     wT: list                        # per block: (qkv, proj, fc1, fc2) weights in `dtype`
+    side: bool = True               # weight gradients on the side stream
 
 
 PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
@@ -85,6 +133,7 @@ class TransformerStackFn(torch.autograd.Function):
         params = ctx.params
         grads = [None] * len(params)
         rb = K.ReduceBatch()
+        wq = WgradQueue(gy.device, spec.side)
         g = gy.reshape(M, D)
         if not g.is_contiguous():
             g = g.contiguous()
@@ -102,12 +151,12 @@ class TransformerStackFn(torch.autograd.Function):
             gi[11] = rb.add(cpart)
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
             dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
-            gi[10] = K.linear_wgrad(gT, a)
+            gi[10] = wq.wgrad(gT, a)
             del a, dgelu
             # mlp.fc1
             gi[9] = rb.add(dA_part)
             dh2 = K.linear_dgrad(dA, w1)
-            gi[8] = K.linear_wgrad(dA, h2)
+            gi[8] = wq.wgrad(dA, h2)
             del dA
             # norm2 (+ residual gradient)
             dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True)
@@ -117,13 +166,13 @@ class TransformerStackFn(torch.autograd.Function):
             # attn.proj
             gi[5] = rb.add(pc)
             dO = K.linear_dgrad(dx1T, wproj)
-            gi[4] = K.linear_wgrad(dx1T, o)
+            gi[4] = wq.wgrad(dx1T, o)
             # attention
             dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
             del dO
             gi[3] = rb.add(qpart)
             dh1 = K.linear_dgrad(dqkv, wqkv)
-            gi[2] = K.linear_wgrad(dqkv, h1)
+            gi[2] = wq.wgrad(dqkv, h1)
             del dqkv
             # norm1 (+ residual gradient)
             dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True)
@@ -133,6 +182,7 @@ class TransformerStackFn(torch.autograd.Function):
             for j in range(PER_BLOCK):
                 grads[i * PER_BLOCK + j] = gi[j].view(p[j].shape)
         rb.flush()
+        wq.join()
         ctx.saved = None
         return (g.view(B, n, D), None, *grads)
 
@@ -288,6 +338,7 @@ class MaeHeadLossFn(torch.autograd.Function):
 class ProjSpec:
     p_drop: float
     seed: int
+    step_ptr: torch.Tensor = None   # device step counter (dropout mask of the current step)
 
 
 class ProjectionHeadFn(torch.autograd.Function):
@@ -301,10 +352,13 @@ class ProjectionHeadFn(torch.autograd.Function):
         g = K.linear_fwd(x, wp, bp, epilogue=K.EPI_GELU, aux_out=pre)
         f = K.linear_fwd(g, wf, bf)
         out, m, r, _, z = K.ln_fwd(f, lw, lb, 1e-5, out_dtype=torch.float32, res=pre, in_dropout=spec.p_drop,
-                                   seed_in=spec.seed, xsum=True)
+                                   seed_in=spec.seed, xsum=True, step_ptr=spec.step_ptr)
         ctx.save = (x, pre, g, z, m, r)
         ctx.w = (wp, wf, lw)
         ctx.spec = spec
+        # the step counter advances at the end of the forward: the backward
+        # re-draws this forward's dropout mask from a snapshot of the step
+        ctx.step_snap = spec.step_ptr.clone() if (spec.step_ptr is not None and spec.p_drop > 0) else None
         return out
 
     @staticmethod
@@ -313,7 +367,7 @@ class ProjectionHeadFn(torch.autograd.Function):
         wp, wf, lw = ctx.w
         spec = ctx.spec
         dz, _, pg, pb, _ = K.ln_bwd(gout.contiguous(), z, m, r, lw)
-        df = K.dropout(dz, spec.p_drop, spec.seed) if spec.p_drop > 0 else dz
+        df = K.dropout(dz, spec.p_drop, spec.seed, step_ptr=ctx.step_snap) if spec.p_drop > 0 else dz
         dwf = K.linear_wgrad(df, g)
         dbf = _reduce(K.rows_colsum(df))
         dpre = K.linear_dgrad(df, wf, out_dtype=torch.float32, epilogue=K.EPI_DGELU, aux=pre, resid=dz)

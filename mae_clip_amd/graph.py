@@ -1,0 +1,79 @@
+"""Whole-training-step HIP graph: forward + backward + AdamW captured once and
+replayed (DESIGN.md §5 "Host").
+
+main.py's loop (main.py:54-66) issues ~600 kernel launches per step through
+Python; at ViT-B/16 shapes the host falls behind the GPU in the backward and
+at every step boundary. CapturedStep runs the first step eagerly (it also
+creates the optimizer state, the bf16 weight shadows and the multi-tensor
+descriptor arrays), captures the second one into a torch.cuda.CUDAGraph (the
+side stream of the text tower / weight gradients joins the capture through its
+events) and replays that graph for every later step: one launch per step.
+
+Everything that changes from step to step is device-resident, so a replay is
+a faithful training step: the MAE mask noise and every dropout mask are keyed
+by CLIPModel.step_counter, AdamW's bias corrections by AdamW._step_dev, and
+both counters are advanced by kernels inside the graph. Batch tensors are
+copied into static input buffers before each replay.
+
+Usage (drop-in around the reference's train_epoch body):
+    runner = CapturedStep(model, optimizer)
+    for batch in loader:
+        loss = runner.step(batch)      # model(batch); loss.backward(); optimizer.step()
+"""
+from __future__ import annotations
+
+import torch
+
+
+class CapturedStep:
+    def __init__(self, model, optimizer, enabled: bool = True, eager_steps: int = 1):
+        self.model = model
+        self.opt = optimizer
+        self.enabled = enabled
+        self.eager_steps = max(1, eager_steps)
+        self.graph = None
+        self.static = None
+        self.loss = None
+        self.calls = 0
+
+    def _eager(self, batch):
+        self.opt.zero_grad(set_to_none=True)
+        loss = self.model(batch)
+        loss.backward()
+        self.opt.step()
+        # detached: a caller holding the loss must not keep this step's autograd
+        # graph (and its AccumulateGrad nodes, bound to the eager stream) alive
+        # into the capture
+        return loss.detach()
+
+    def _capture(self, batch):
+        self.static = {k: v.clone() for k, v in batch.items()}
+        model_step = self.model.step
+        # grads are re-created inside the graph's private pool: drop the eager ones
+        self.opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="relaxed"):
+            loss = self.model(self.static)
+            loss.backward()
+            self.opt.step()
+        # capture recorded the work without running it: undo its host-side counting
+        self.model.step = model_step
+        self.opt._advance_host_steps(-1)
+        self.graph, self.loss = g, loss
+
+    def step(self, batch):
+        """One training step on `batch` (dict of device tensors); returns the loss tensor."""
+        self.calls += 1
+        if not self.enabled or self.calls <= self.eager_steps:
+            return self._eager(batch)
+        if self.graph is None:
+            self._capture(batch)
+        else:
+            for k, v in batch.items():
+                if v.data_ptr() != self.static[k].data_ptr():
+                    self.static[k].copy_(v, non_blocking=True)
+        self.graph.replay()
+        self.model.step += 1
+        self.opt._advance_host_steps(1)
+        return self.loss

@@ -61,6 +61,11 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
                    alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
                    resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum), splitk=splitk,
                    workspace=_ptr(workspace))
+    if workspace is None and A.dtype == torch.float32:
+        nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
+        if nb > 0:
+            workspace = torch.empty((nb // 4,), device=A.device, dtype=torch.float32)
+            a.workspace = workspace.data_ptr()
     if LAUNCH_HOOK is None:
         _call("maeclip_gemm", C.byref(a), _stream())
     else:
@@ -142,10 +147,11 @@ def pool_bwd(dout, n, dx=None, accumulate=False):
     return dx
 
 
-def dropout(x, p, seed, out=None):
+def dropout(x, p, seed, out=None, step_ptr=None):
     M, D = x.shape
     out = out if out is not None else torch.empty_like(x)
-    _call("maeclip_dropout", x.data_ptr(), out.data_ptr(), M, D, x.stride(0), float(p), int(seed), _stream())
+    _call("maeclip_dropout", x.data_ptr(), out.data_ptr(), M, D, x.stride(0), float(p), int(seed), _ptr(step_ptr),
+          _stream())
     return out
 
 
@@ -160,7 +166,7 @@ def embed_fwd(ids, word, pos):
 
 # -------------------------------------------------------------- LayerNorm
 def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dropout=0.0, seed_in=0, seed_out=0,
-           want_stats=True, y2=False, xsum=False):
+           want_stats=True, y2=False, xsum=False, step_ptr=None):
     """Returns (y, mean, rstd, y2_bf16, xsum)."""
     _dev(x, gamma, beta, res)
     M, D = x.shape
@@ -173,7 +179,7 @@ def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dr
     a = L.LnFwdArgs(x=x.data_ptr(), x_dtype=_dt(x), res=_ptr(res), ldres=(res.stride(0) if res is not None else 0),
                     in_dropout_p=in_dropout, gamma=gamma.data_ptr(), beta=beta.data_ptr(), y=y.data_ptr(),
                     y_dtype=_dt(y), y2=_ptr(yb), ldy2=D, xsum_out=_ptr(xs), ldxs=D, mean=_ptr(mean), rstd=_ptr(rstd),
-                    out_dropout_p=out_dropout, seed_in=int(seed_in), seed_out=int(seed_out),
+                    out_dropout_p=out_dropout, seed_in=int(seed_in), seed_out=int(seed_out), step_ptr=_ptr(step_ptr),
                     M=M, D=D, ldx=x.stride(0), ldy=D, eps=eps)
     _call("maeclip_ln_fwd", C.byref(a), _stream())
     return y, mean, rstd, yb, xs
@@ -203,14 +209,14 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
 
 
 # -------------------------------------------------------------- attention
-def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True):
+def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True, step_ptr=None):
     _dev(qkv, key_mask)
     D = H * hd
     o = torch.empty((B * n, D), device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty((B, H, n), device=qkv.device, dtype=torch.float32) if want_lse else None
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=_ptr(lse), dout=None, dqkv=None, key_mask=_ptr(key_mask),
                    colsum_partial=None, ld_qkv=qkv.stride(0), ld_o=D, ld_dqkv=0, B=B, n=n, H=H, head_dim=hd,
-                   dtype=_dt(qkv), scale=scale, dropout_p=dropout_p, seed=int(seed))
+                   dtype=_dt(qkv), scale=scale, dropout_p=dropout_p, seed=int(seed), step_ptr=_ptr(step_ptr))
     _call("maeclip_attn_fwd", C.byref(a), _stream())
     return o, lse
 
@@ -228,14 +234,15 @@ def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True):
 
 
 # --------------------------------------------------------------------- MAE
-def mask_ids(B, L_, len_keep, seed, step, sample_offset, device, want_noise=False):
+def mask_ids(B, L_, len_keep, seed, step, sample_offset, device, want_noise=False, step_ptr=None):
+    """HF random_masking ids for mask step `step` (+ *step_ptr when given)."""
     ids_shuffle = torch.empty((B, L_), device=device, dtype=torch.int32)
     ids_restore = torch.empty((B, L_), device=device, dtype=torch.int32)
     mask = torch.empty((B, L_), device=device, dtype=torch.float32)
     noise = torch.empty((B, L_), device=device, dtype=torch.float32) if want_noise else None
     a = L.MaskArgs(ids_shuffle=ids_shuffle.data_ptr(), ids_restore=ids_restore.data_ptr(), mask=mask.data_ptr(),
                    noise=_ptr(noise), B=B, L=L_, len_keep=len_keep, seed=int(seed), step=int(step),
-                   sample_offset=int(sample_offset))
+                   sample_offset=int(sample_offset), step_ptr=_ptr(step_ptr))
     _call("maeclip_mask_ids", C.byref(a), _stream())
     return ids_shuffle, ids_restore, mask, noise
 
@@ -337,17 +344,39 @@ def clip_loss(I, T, temperature, want_grad=True):
 
 
 # ------------------------------------------------------------ multi-tensor
+def counter_add(counter, delta=1):
+    """counter (device int64[1]) += delta, stream-ordered (graph-capturable)."""
+    _dev(counter)
+    _call("maeclip_counter_add", counter.data_ptr(), int(delta), _stream())
+
+
+def _capturing() -> bool:
+    return torch.cuda.is_current_stream_capturing()
+
+
 class PinnedStager:
     """Host -> device staging of small descriptor arrays through a ring of pinned
-    buffers; a buffer is reused only after the async copy that read it is done."""
+    buffers; a buffer is reused only after the async copy that read it is done.
+
+    Under HIP-graph capture the copy becomes a memcpy node that re-reads its
+    pinned source at every replay, so each captured stage gets a pinned buffer
+    of its own that is never rewritten (kept in `captured` for the graph's life)."""
 
     def __init__(self, slots=4):
         self.bufs = [None] * slots
         self.events = [None] * slots
         self.k = 0
+        self.captured = []
 
     def stage(self, host_struct_array, device):
         nbytes = C.sizeof(host_struct_array)
+        if _capturing():
+            pin = torch.empty(max(nbytes, 16), dtype=torch.uint8).pin_memory()
+            pin[:nbytes].numpy()[:] = memoryview(host_struct_array).cast("B")
+            dev = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+            _call("maeclip_memcpy_h2d", dev.data_ptr(), pin.data_ptr(), nbytes, _stream())
+            self.captured.append(pin)
+            return dev
         k = self.k
         self.k = (k + 1) % len(self.bufs)
         if self.events[k] is not None:
@@ -419,9 +448,10 @@ def cast_multi(plan: MultiTensorPlan):
     _call("maeclip_cast_multi", plan.dev.data_ptr(), plan.host, plan.n, _stream())
 
 
-def adamw_multi(plan: MultiTensorPlan, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
-    bc1 = 1.0 - beta1 ** step
-    bc2 = 1.0 - beta2 ** step
+def adamw_multi(plan: MultiTensorPlan, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, step_ptr=None):
+    """step: host step count t (>= 1), or step_ptr: device int64 holding t."""
+    bc1 = 1.0 - beta1 ** max(step, 1)
+    bc2 = 1.0 - beta2 ** max(step, 1)
     hp = L.AdamwHparams(lr=lr, beta1=beta1, beta2=beta2, eps=eps, weight_decay=weight_decay, step_size=lr / bc1,
-                        bc2_sqrt=bc2 ** 0.5, grad_scale=grad_scale)
+                        bc2_sqrt=bc2 ** 0.5, grad_scale=grad_scale, step_ptr=_ptr(step_ptr))
     _call("maeclip_adamw_multi", plan.dev.data_ptr(), plan.host, plan.n, C.byref(hp), _stream())

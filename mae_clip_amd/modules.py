@@ -140,7 +140,8 @@ class Block(nn.Module):
 def run_stack(blocks, x, heads, dtype, cache: WeightCache):
     B, n, D = x.shape
     wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in blocks]
-    spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=blocks[0].norm1.eps, dtype=dtype, wT=wT)
+    spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=blocks[0].norm1.eps, dtype=dtype, wT=wT,
+                        side=bool(CFG.side_stream))
     params = [p for blk in blocks for p in blk.stack_params()]
     return Fn.TransformerStackFn.apply(x, spec, *params)
 
@@ -328,7 +329,7 @@ class DistilBertModel(nn.Module):
         return self._wc
 
     @torch.no_grad()
-    def forward(self, input_ids, attention_mask, dtype=None, seed=0):
+    def forward(self, input_ids, attention_mask, dtype=None, seed=0, step_ptr=None):
         """Returns last_hidden_state [B, T, dim] (f32)."""
         _require_device(input_ids, "input_ids")
         dtype = dtype or compute_dtype(self.precision)
@@ -344,12 +345,13 @@ class DistilBertModel(nn.Module):
         emb = self.embeddings
         x = K.embed_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight)
         h, _, _, hT, _ = K.ln_fwd(x, emb.LayerNorm.weight, emb.LayerNorm.bias, 1e-12, out_dtype=torch.float32,
-                                  out_dropout=pdrop, seed_out=seed * 131 + 1, want_stats=False, y2=bf)
+                                  out_dropout=pdrop, seed_out=seed * 131 + 1, want_stats=False, y2=bf,
+                                  step_ptr=step_ptr)
         hT = hT if bf else h
         for li, (lyr, (wqkv, bqkv, wout, w1, w2)) in enumerate(zip(self.transformer.layer, self._weights(dtype))):
             qkv = K.linear_fwd(hT, wqkv, bqkv)
             o, _ = K.attn_fwd(qkv, B, T, H, hd, hd ** -0.5, key_mask=am, dropout_p=padrop,
-                              seed=seed * 131 + 7 * li + 2, want_lse=False)
+                              seed=seed * 131 + 7 * li + 2, want_lse=False, step_ptr=step_ptr)
             sa = K.linear_fwd(o, wout, lyr.attention.out_lin.bias, out_dtype=torch.float32)
             a, _, _, aT, _ = K.ln_fwd(sa, lyr.sa_layer_norm.weight, lyr.sa_layer_norm.bias, 1e-12,
                                       out_dtype=torch.float32, res=h, want_stats=False, y2=bf)
@@ -358,7 +360,7 @@ class DistilBertModel(nn.Module):
             f2 = K.linear_fwd(f1, w2, lyr.ffn.lin2.bias, out_dtype=torch.float32)
             h, _, _, hT, _ = K.ln_fwd(f2, lyr.output_layer_norm.weight, lyr.output_layer_norm.bias, 1e-12,
                                       out_dtype=torch.float32, res=a, in_dropout=pdrop, seed_in=seed * 131 + 7 * li + 3,
-                                      want_stats=False, y2=bf)
+                                      want_stats=False, y2=bf, step_ptr=step_ptr)
             hT = hT if bf else h
         return h.view(B, T, D)
 
@@ -379,8 +381,9 @@ class TextEncoder(nn.Module):
             p.requires_grad = trainable
         self.target_token_idx = 0
 
-    def forward(self, input_ids, attention_mask, seed=0, dtype=None):
-        last_hidden_state = self.model(input_ids=input_ids, attention_mask=attention_mask, seed=seed, dtype=dtype)
+    def forward(self, input_ids, attention_mask, seed=0, dtype=None, step_ptr=None):
+        last_hidden_state = self.model(input_ids=input_ids, attention_mask=attention_mask, seed=seed, dtype=dtype,
+                                       step_ptr=step_ptr)
         return last_hidden_state[:, self.target_token_idx, :]
 
 
@@ -398,10 +401,10 @@ class ProjectionHead(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.layer_norm = nn.LayerNorm(projection_dim)
 
-    def forward(self, x, seed=0):
+    def forward(self, x, seed=0, step_ptr=None):
         _require_device(x, "projection input")
         p = self.dropout.p if self.training else 0.0
-        spec = Fn.ProjSpec(p_drop=p, seed=seed)
+        spec = Fn.ProjSpec(p_drop=p, seed=seed, step_ptr=step_ptr)
         return Fn.ProjectionHeadFn.apply(x, spec, self.projection.weight, self.projection.bias, self.fc.weight,
                                          self.fc.bias, self.layer_norm.weight, self.layer_norm.bias)
 

@@ -1,8 +1,14 @@
 """Fused multi-tensor AdamW on the libmaeclip kernel.
 
 Same update as torch.optim.AdamW (main.py:101-103: lr 1e-3, weight_decay 1e-3,
-betas (0.9, 0.999), eps 1e-8), one kernel launch for all parameters. It
-optionally refreshes a model's bf16 weight shadows in the same pass.
+betas (0.9, 0.999), eps 1e-8), one kernel launch for all parameters.
+
+The step count t lives on the device as well (`_step_dev`, advanced by a
+kernel before the update and read by it for the bias corrections), so the
+optimizer step can be captured into a HIP graph together with the forward and
+backward (mae_clip_amd.graph.CapturedStep). The per-parameter host
+state["step"] is kept equal to it (state_dict / load_state_dict compatible
+with torch.optim.AdamW).
 """
 from __future__ import annotations
 
@@ -16,12 +22,12 @@ class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
-        self._pinned = [None, None]
-        self._events = [None, None]
-        self._flip = 0
+        self._stager = K.PinnedStager(slots=2)
+        self._step_dev = None     # device int64[1]: step count t of the uniform-step path
+        self._dev_mirror = 0      # host copy of the value *_step_dev will hold when the stream gets there
 
     def _plan(self, entries, device):
-        """Entry array staged through alternating pinned buffers (async H2D)."""
+        """Entry array staged through the pinned stager (async H2D, capturable)."""
         chunk = int(L.lib().maeclip_mt_chunk())
         n = len(entries)
         host = (L.MtEntry * n)()
@@ -32,23 +38,18 @@ class AdamW(torch.optim.Optimizer):
             h.n = e[5]
             h.chunk_start = start
             start += (e[5] + chunk - 1) // chunk
-        nbytes = C_sizeof(host)
-        k = self._flip
-        self._flip ^= 1
-        if self._events[k] is not None:
-            self._events[k].synchronize()  # the H2D copy that last read this buffer is done
-        buf = self._pinned[k]
-        if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-            self._pinned[k] = buf
-        buf[:nbytes].numpy()[:] = memoryview(host).cast("B")
-        dev = buf[:nbytes].to(device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._events[k] = ev
         plan = K.MultiTensorPlan.__new__(K.MultiTensorPlan)
-        plan.host, plan.dev, plan.n = host, dev, n
+        plan.host, plan.dev, plan.n = host, self._stager.stage(host, device), n
         return plan
+
+    def _device_step(self, t, device):
+        """Advance the device step counter to t (normally +1) on the stream."""
+        if self._step_dev is None or self._step_dev.device != device:
+            self._step_dev = torch.zeros(1, dtype=torch.int64, device=device)
+            self._dev_mirror = 0
+        K.counter_add(self._step_dev, t - self._dev_mirror)
+        self._dev_mirror = t
+        return self._step_dev
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -69,23 +70,30 @@ class AdamW(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["step"] += 1
+                st["step"] = int(st["step"]) + 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 entries.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                                 None, p.numel(), st["step"]))
                 device = p.device
             if not entries:
                 continue
-            # all parameters of a group share the step count after the first step
-            steps = {e[6] for e in entries}
             b1, b2 = group["betas"]
-            for s in sorted(steps):
-                sub = [e[:6] for e in entries if e[6] == s]
-                plan = self._plan(sub, device)
-                K.adamw_multi(plan, group["lr"], b1, b2, group["eps"], group["weight_decay"], s)
+            steps = sorted({e[6] for e in entries})
+            if len(steps) == 1:
+                # every parameter at the same t (the training loop's case): t on the device
+                t = steps[0]
+                plan = self._plan([e[:6] for e in entries], device)
+                K.adamw_multi(plan, group["lr"], b1, b2, group["eps"], group["weight_decay"], t,
+                              step_ptr=self._device_step(t, device))
+            else:
+                for s in steps:
+                    plan = self._plan([e[:6] for e in entries if e[6] == s], device)
+                    K.adamw_multi(plan, group["lr"], b1, b2, group["eps"], group["weight_decay"], s)
         return loss
 
-
-def C_sizeof(obj):
-    import ctypes
-    return ctypes.sizeof(obj)
+    def _advance_host_steps(self, delta):
+        """Host bookkeeping for graph replays / capture (no kernel launched)."""
+        for st in self.state.values():
+            if "step" in st:
+                st["step"] = int(st["step"]) + delta
+        self._dev_mirror += delta

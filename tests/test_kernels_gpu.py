@@ -21,7 +21,8 @@ def _ref_mm(A, B):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("lay", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("mnk", [(256, 256, 128), (200, 136, 72), (16, 8, 64), (384, 640, 1024), (264, 520, 64), (520, 264, 192)])
+@pytest.mark.parametrize("mnk", [(256, 256, 128), (200, 136, 72), (16, 8, 64), (384, 640, 1024), (264, 520, 64), (520, 264, 192),
+                                 (640, 520, 256)])
 def test_gemm_layouts(dev, dtype, lay, mnk):
     M, N, Kd = mnk
     a_lay, b_lay = lay
@@ -38,8 +39,9 @@ def test_gemm_layouts(dev, dtype, lay, mnk):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogues(dev, dtype):
-    M, N, Kd = 300, 384, 256
+@pytest.mark.parametrize("M", [300, 700])   # fp32: 32x32-tile small kernel / 128x128 MFMA kernel
+def test_gemm_epilogues(dev, dtype, M):
+    N, Kd = 384, 256
     x = _rand((M, Kd), dtype, dev, seed=3)
     w = _rand((N, Kd), dtype, dev, scale=0.05, seed=4)
     bias = _rand((N,), torch.float32, dev, seed=5)
