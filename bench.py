@@ -101,6 +101,26 @@ def cpu_baseline(seconds_budget=20.0):
                       f"step(s) after 1 warm-up (fwd+bwd+AdamW)"}
 
 
+def pmc_traffic(key):
+    """HBM bytes per launch of GEMM shape `key` from the committed rocprofv3 PMC
+    summaries (profiles/*/traffic_*.json, written by tools/pmc_traffic.sh:
+    FETCH_SIZE x 2 + WRITE_SIZE, separate passes, MI355X_MICROARCH.md §HBM).
+    PMC counters cannot be read inside a timed run, so the newest matching file
+    is reported with its path; None when no summary covers the shape."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
+        try:
+            r = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if r.get("shape") == key and (best is None or os.path.getmtime(f) >= os.path.getmtime(best[0])):
+            best = (f, r)
+    if best is None:
+        return None, None
+    return best[1]["hbm_bytes"], os.path.relpath(best[0], ROOT)
+
+
 class KernelTimer:
     """Brackets GEMM launches with HIP events on the launching stream; reports
     the shape with the largest total time.
@@ -188,6 +208,8 @@ def main():
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one HIP graph per step")
     ap.add_argument("--gemm-table", action="store_true", help="per-shape GEMM times to stderr")
+    ap.add_argument("--no-side-stream", action="store_true",
+                    help="text tower and weight gradients on the main stream (config.side_stream = False)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,7 +227,8 @@ def main():
 
     model = build_model(dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6,
                              mask_ratio=args.mask_ratio, decoder_embed_dim=512, decoder_depth=8,
-                             decoder_num_heads=16, precision="bf16")).to(device)
+                             decoder_num_heads=16, precision="bf16",
+                             side_stream=not args.no_side_stream)).to(device)
     model.train()
     dp = DataParallel(model) if world > 1 else None
     opt = AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
@@ -276,9 +299,11 @@ def main():
             key, flops, tot_ms, nl = best
             avg_s = tot_ms / nl / 1000.0
             ach = flops / avg_s / 1e12
+            traffic, tsrc = pmc_traffic(key)
             roof = {"bound": "mfma", "kernel": "gemm " + key, "achieved": round(ach, 1),
                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                    "traffic": None, "avg_launch_us": round(avg_s * 1e6, 1), "launches": nl,
+                    "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+                    "avg_launch_us": round(avg_s * 1e6, 1), "launches": nl,
                     "step_tflops": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12, 1),
                     "step_frac": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12 / PEAK_BF16_TFLOPS, 4)}
         out = {"metric": "images/sec/node ViT-B/16 CLIP+MAE step", "value": round(value, 2), "unit": "images/s",

@@ -88,6 +88,28 @@ int64_t maeclip_gemm_colsum_rows(int64_t M);
 int64_t maeclip_gemm_workspace(const maeclip_gemm_args* args);
 int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K);
 
+/* Grouped weight gradients. Replaces the weight-gradient half of autograd's
+ * nn.Linear backward (torch.nn.functional.linear's backward, reached from
+ * loss.backward() at main.py:58) for all Linears of a transformer stack at
+ * once (timm Block qkv/proj/fc1/fc2, HF ViTMAE decoder layers):
+ *   dw_p[n][k] = sum_m dy_p[m*ldy + n] * x_p[m*ldx + k]  (+ beta * dw_p[n][k])
+ * for p < nprob, m < M (tokens, shared by every problem). dw is fp32 dense
+ * [N][K]; dy/x have `dtype`. bf16 problems with M % 64 == 0 and N, K >= 256
+ * share one persistent launch per 48 problems (no split-K slab unless the tile
+ * count leaves > 20% of the CUs idle); others run one maeclip_gemm each.
+ * Deterministic (fixed summation order). workspace: >= the bytes
+ * maeclip_wgrad_grouped_workspace() returns (0 is common), 16-B aligned. */
+typedef struct {
+  const void* dy;
+  const void* x;
+  float* dw;
+  int64_t N, K, ldy, ldx;
+} maeclip_wgrad_problem;
+int64_t maeclip_wgrad_grouped_workspace(const maeclip_wgrad_problem* probs, int32_t nprob, int64_t M,
+                                        int32_t dtype);
+int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int32_t nprob, int64_t M, int32_t dtype,
+                              float beta, void* workspace, int64_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------- attention
  * Replaces F.scaled_dot_product_attention in timm Attention / HF ViTMAE
  * decoder layers and DistilBERT attention with key-padding mask

@@ -145,9 +145,16 @@ class CLIPModel(nn.Module):
             xd = Fn.DecoderEmbedFn.apply(latent, ids_shuffle, ids_restore, dspec, dec.decoder_embed.weight,
                                          dec.decoder_embed.bias, dec.mask_token, dec.decoder_pos_embed)
             xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache)
+            wp_T, bp_pad = cache.get(dec.decoder_pred.weight, dtype), None
+            P = wp_T.shape[0]
+            if dtype == torch.bfloat16 and P % 64:
+                # p*p*C = 588 at patch 14: pad decoder_pred's output rows to a
+                # multiple of 64 (16-B rows for every GEMM of the head); zero
+                # weight rows / bias entries, pred's pad columns are never read
+                wp_T, bp_pad = dec.padded_pred(wp_T)
             hspec = Fn.MaeHeadSpec(p=vit.patch_embed.patch_size, norm_pix=self.norm_pix_loss,
                                    mask_count=float(B * (L - keep)), loss_scale=1.0 / world, dtype=dtype,
-                                   w_T=cache.get(dec.decoder_pred.weight, dtype))
+                                   w_T=wp_T, b_pad=bp_pad)
             ml = Fn.MaeHeadLossFn.apply(xd, img if img.dtype == torch.float32 else img.float(), mask, hspec,
                                         dec.decoder_norm.weight, dec.decoder_norm.bias, dec.decoder_pred.weight,
                                         dec.decoder_pred.bias)

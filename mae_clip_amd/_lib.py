@@ -107,6 +107,10 @@ class ClipArgs(C.Structure):
                 ("ld_dI", c_i64), ("ld_dT", c_i64), ("workspace", c_vp), ("ws_bytes", c_sz)]
 
 
+class WgradProblem(C.Structure):
+    _fields_ = [("dy", c_vp), ("x", c_vp), ("dw", c_vp), ("N", c_i64), ("K", c_i64), ("ldy", c_i64), ("ldx", c_i64)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "maeclip_abi_version": (c_i32, []),
@@ -116,6 +120,8 @@ _SIGS = {
     "maeclip_gemm_colsum_rows": (c_i64, [c_i64]),
     "maeclip_gemm_workspace": (c_i64, [C.POINTER(GemmArgs)]),
     "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
+    "maeclip_wgrad_grouped_workspace": (c_i64, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32]),
+    "maeclip_wgrad_grouped": (c_i32, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32, c_f32, c_vp, c_i64, c_vp]),
     "maeclip_attn_fwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_attn_bwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_ln_fwd": (c_i32, [C.POINTER(LnFwdArgs), c_vp]),

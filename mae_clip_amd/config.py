@@ -68,3 +68,4 @@ mask_seed = 2
 dropout_seed = 1234
 # ---- scheduling
 side_stream = True         # frozen text tower || image encoder; weight-gradient GEMMs || the dgrad chain
+wgrad_grouped = True       # all weight gradients of a stack in one grouped GEMM launch (maeclip_wgrad_grouped)

@@ -147,15 +147,11 @@ __device__ __forceinline__ void swap_pairs(v4f (&acc)[8][4]) {
       }
 }
 
-// split-K slab: fp32 partial of this K slice, no epilogue
-__device__ __forceinline__ void epilogue4_slab(const maeclip_gemm_args& args, v4f (&acc)[8][4], int64_t z, int m0,
-                                               int n0, int wm, int wn, int lane) {
-  const int M = (int)args.M, N = (int)args.N;
+// split-K slab: fp32 partial of this K slice (dense [M, N]), no epilogue
+__device__ __forceinline__ void epilogue4_slab(float* __restrict__ slab, int M, int N, float alpha, v4f (&acc)[8][4],
+                                               int m0, int n0, int wm, int wn, int lane) {
   const int g = lane >> 4;
-  const int S = args.splitk;
   swap_pairs(acc);
-  float* slab = args.workspace + ((int64_t)z * S + blockIdx.y) * (int64_t)M * N;
-  const float alpha = args.alpha;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + 128 * wm + 64 * (i >> 2) + 16 * (i & 3) + (lane & 15);
@@ -328,73 +324,145 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
   }
 }
 
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT>
-__global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
+// One unit of work of the persistent loop: a 256x256 output tile of one
+// problem and its K range (a split-K slice or the whole K).
+struct Unit4 {
+  const bf16_t* A;
+  const bf16_t* B;
+  int64_t lda, ldb;
+  int M, N, K;        // problem sizes (K = full reduction length)
+  int m0, n0;
+  int kbeg, nt;       // first k and number of 64-wide K-tiles of this unit
+  int slice, prob;
+};
+
+// Grouped weight gradients (maeclip_wgrad_grouped): dW_p[N_p, K_p] (+)=
+// dy_p[Mtok, N_p]^T x_p[Mtok, K_p] for up to WG_MAX problems in one persistent
+// launch, so the 4 x layers weight-gradient GEMMs of a transformer stack share
+// one grid instead of each needing an fp32 split-K slab round trip to fill the
+// chip. In GEMM terms M = N_p, N = K_p, K = Mtok, both operands RC.
+constexpr int WG_MAX = 48;
+struct WgProb {
+  const bf16_t* dy;
+  const bf16_t* x;
+  float* dw;
+  int N, K, ldy, ldx;
+  int tile_begin;     // prefix sum of tiles
+  int slab_off;       // floats, S > 1 only
+};
+struct WgGroup {
+  int np, S, T, Mtok;
+  float beta;
+  float* ws;
+  WgProb p[WG_MAX];
+};
+
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP>
+__device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int M = (int)args.M, N = (int)args.N, K = (int)args.K;
+  const int64_t z = GRP ? 0 : blockIdx.z;
 
-  const int gm = (M + 255) / 256, gn = (N + 255) / 256;
-  const int T = gm * gn;
-  // Persistent over output tiles: the tiles are cut into 8 contiguous chunks,
-  // chunk x worked by the blocks with blockIdx.x % 8 == x (round-robin
-  // dispatch puts them on one XCD, so concurrently running tiles share A rows
-  // in that XCD's L2; placement is a speed assumption only).
+  // units: standard = output tiles (this block's slice is blockIdx.y);
+  // grouped = slice-major (slice, tile) pairs, so neighbouring units share operands
+  int T, gn = 1, klen = 0;
+  if (GRP) {
+    T = gp->T * gp->S;
+    klen = ((gp->Mtok + gp->S - 1) / gp->S + 63) / 64 * 64;
+  } else {
+    const int gm = ((int)args.M + 255) / 256;
+    gn = ((int)args.N + 255) / 256;
+    T = gm * gn;
+    const int S = SPLIT ? args.splitk : 1;
+    klen = (((int)args.K + S - 1) / S + 63) / 64 * 64;
+  }
+  auto unit = [&](int u) {
+    Unit4 w;
+    if (GRP) {
+      const int tile = u % gp->T, sl = u / gp->T;
+      int p = 0;
+      while (p + 1 < gp->np && gp->p[p + 1].tile_begin <= tile) ++p;
+      const WgProb& q = gp->p[p];
+      const int local = tile - q.tile_begin, gnp = (q.K + 255) / 256;
+      w.A = q.dy;
+      w.B = q.x;
+      w.lda = q.ldy;
+      w.ldb = q.ldx;
+      w.M = q.N;
+      w.N = q.K;
+      w.K = gp->Mtok;
+      w.m0 = (local / gnp) * 256;
+      w.n0 = (local % gnp) * 256;
+      w.slice = sl;
+      w.prob = p;
+    } else {
+      w.A = (const bf16_t*)args.A + z * args.strideA;
+      w.B = (const bf16_t*)args.B + z * args.strideB;
+      w.lda = args.lda;
+      w.ldb = args.ldb;
+      w.M = (int)args.M;
+      w.N = (int)args.N;
+      w.K = (int)args.K;
+      w.m0 = (u / gn) * 256;
+      w.n0 = (u % gn) * 256;
+      w.slice = blockIdx.y;
+      w.prob = 0;
+    }
+    w.kbeg = w.slice * klen;
+    const int kend = min(w.K, w.kbeg + klen);
+    w.nt = kend > w.kbeg ? (kend - w.kbeg) / 64 : 0;
+    return w;
+  };
+
+  // Persistent over units: the units are cut into 8 contiguous chunks, chunk
+  // x worked by the blocks with blockIdx.x % 8 == x (round-robin dispatch puts
+  // them on one XCD, so concurrently running tiles share A rows in that XCD's
+  // L2; placement is a speed assumption only).
   const int G = gridDim.x, x8 = blockIdx.x % 8, li = blockIdx.x / 8;
   const int nbx = (G - x8 + 7) / 8;
   const int cq = T / 8, cr = T % 8;
   const int cbeg = x8 < cr ? x8 * (cq + 1) : cr * (cq + 1) + (x8 - cr) * cq;
   const int cend = cbeg + cq + (x8 < cr ? 1 : 0);
 
-  const int64_t z = blockIdx.z;
-  const bf16_t* __restrict__ A = (const bf16_t*)args.A + z * args.strideA;
-  const bf16_t* __restrict__ B = (const bf16_t*)args.B + z * args.strideB;
-  const int64_t lda = args.lda, ldb = args.ldb;
-
-  const int S = SPLIT ? args.splitk : 1;
-  const int klen = ((K + S - 1) / S + 63) / 64 * 64;
-  const int kbeg = blockIdx.y * klen;
-  const int kend = min(K, kbeg + klen);
-  const int nt = kend > kbeg ? (kend - kbeg) / 64 : 0;
-
-  // per-lane DMA offsets, invariant over tiles and K-tiles
-  int voA[2][2], voB[2][2];
+  // per-lane DMA byte offsets of a unit's operands (loop invariants of its K loop)
+  auto offsets = [&](const Unit4& w, int (&vA)[2][2], int (&vB)[2][2]) {
 #pragma unroll
-  for (int sub = 0; sub < 2; ++sub)
+    for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      voA[sub][i] = half_voffset<LA, true>(lda, sub, i, wave, lane);
-      voB[sub][i] = half_voffset<LB, false>(ldb, sub, i, wave, lane);
-    }
-  // K-tile advance in bytes: along the row (KC) or down the k-rows (RC)
-  const int kstepA = LA == LAY_KC ? 2 : (int)(lda * 2), kstepB = LB == LAY_KC ? 2 : (int)(ldb * 2);
-  auto rsrcA = [&](int m0) {
-    return LA == LAY_KC ? make_rsrc(A + (int64_t)m0 * lda, ((int64_t)M - m0) * lda * 2)
-                        : make_rsrc(A + m0, ((int64_t)K * lda - m0) * 2);
+      for (int i = 0; i < 2; ++i) {
+        vA[sub][i] = half_voffset<LA, true>(w.lda, sub, i, wave, lane);
+        vB[sub][i] = half_voffset<LB, false>(w.ldb, sub, i, wave, lane);
+      }
   };
-  auto rsrcB = [&](int n0) {
-    return LB == LAY_KC ? make_rsrc(B + (int64_t)n0 * ldb, ((int64_t)N - n0) * ldb * 2)
-                        : make_rsrc(B + n0, ((int64_t)K * ldb - n0) * 2);
-  };
-  // half h of K-tile t of the tile at (m0, n0): 0 = Am0, 1 = Am1, 2 = Bn0, 3 = Bn1
-  auto issue = [&](int m0, int n0, int t, int h) {
+  // half h of K-tile t of unit w: 0 = Am0, 1 = Am1, 2 = Bn0, 3 = Bn1. The
+  // K-tile advance is along the row (KC) or down the k-rows (RC).
+  auto issue = [&](const Unit4& w, const int (&vA)[2][2], const int (&vB)[2][2], int t, int h) {
     char* dst = smem + (t & 1) * BUF + h * HALF;
-    const int k0 = kbeg + t * 64;
-    if (h < 2) issue_half(rsrcA(m0), voA[h][0], voA[h][1], k0 * kstepA, dst, wave);
-    else issue_half(rsrcB(n0), voB[h - 2][0], voB[h - 2][1], k0 * kstepB, dst, wave);
+    const int k0 = w.kbeg + t * 64;
+    if (h < 2) {
+      const rsrc_t rs = LA == LAY_KC ? make_rsrc(w.A + (int64_t)w.m0 * w.lda, ((int64_t)w.M - w.m0) * w.lda * 2)
+                                     : make_rsrc(w.A + w.m0, ((int64_t)w.K * w.lda - w.m0) * 2);
+      issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? 2 : (int)(w.lda * 2)), dst, wave);
+    } else {
+      const rsrc_t rs = LB == LAY_KC ? make_rsrc(w.B + (int64_t)w.n0 * w.ldb, ((int64_t)w.N - w.n0) * w.ldb * 2)
+                                     : make_rsrc(w.B + w.n0, ((int64_t)w.K * w.ldb - w.n0) * 2);
+      issue_half(rs, vB[h - 2][0], vB[h - 2][1], k0 * (LB == LAY_KC ? 2 : (int)(w.ldb * 2)), dst, wave);
+    }
   };
   // K-tile 0 whole + three halves of K-tile 1 (its Am1 follows in p0)
-  auto prologue = [&](int m0, int n0) {
-    issue(m0, n0, 0, 0);
-    issue(m0, n0, 0, 2);
-    issue(m0, n0, 0, 3);
-    issue(m0, n0, 0, 1);
-    if (nt > 1) {
-      issue(m0, n0, 1, 0);
-      issue(m0, n0, 1, 2);
-      issue(m0, n0, 1, 3);
+  auto prologue = [&](const Unit4& w) {
+    int vA[2][2], vB[2][2];
+    offsets(w, vA, vB);
+    issue(w, vA, vB, 0, 0);
+    issue(w, vA, vB, 0, 2);
+    issue(w, vA, vB, 0, 3);
+    issue(w, vA, vB, 0, 1);
+    if (w.nt > 1) {
+      issue(w, vA, vB, 1, 0);
+      issue(w, vA, vB, 1, 2);
+      issue(w, vA, vB, 1, 3);
     }
   };
 
@@ -411,11 +479,12 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
 #endif
   for (int tile = cbeg + li; tile < cend; tile += nbx) {
     STAMP(0);
-    const int bm = tile / gn, bn = tile % gn;
-    const int m0 = bm * 256, n0 = bn * 256;
+    const Unit4 u = unit(tile);
+    const int m0 = u.m0, n0 = u.n0, nt = u.nt;
     const int tnext = tile + nbx;
-    const int m0n = (tnext / gn) * 256, n0n = (tnext % gn) * 256;
-    if (nt > 0 && !primed) prologue(m0, n0);
+    int voA[2][2], voB[2][2];
+    offsets(u, voA, voB);
+    if (nt > 0 && !primed) prologue(u);
     if (first && nt > 1) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else if (prev_full) {
@@ -430,7 +499,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     first = false;
-    prev_full = !SPLIT && m0 + 256 <= M && n0 + 256 <= N;
+    prev_full = !SPLIT && m0 + 256 <= u.M && n0 + 256 <= u.N;
     primed = false;
     SEG_BARRIER();
     if (wm == 1) SEG_BARRIER();
@@ -459,7 +528,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA0, 64 * wm + 16 * i, ks, lane);
-      if (more1) issue(m0, n0, t + 1, 1);
+      if (more1) issue(u, voA, voB, t + 1, 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
@@ -477,7 +546,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = frag<LB>(hB1, 32 * wn + 16 * j, ks, lane);
-      if (more2) issue(m0, n0, t + 2, 0);
+      if (more2) issue(u, voA, voB, t + 2, 0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
@@ -495,7 +564,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, 64 * wm + 16 * i, ks, lane);
-      if (more2) issue(m0, n0, t + 2, 2);
+      if (more2) issue(u, voA, voB, t + 2, 2);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
@@ -511,15 +580,18 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
       SEG_BARRIER();
       // ---- p3: quadrant (1,0), operands already in VGPRs. Every LDS read of
       // this tile has been retired behind an earlier barrier, so the last
-      // K-tile starts the next output tile's DMA here.
+      // K-tile starts the next unit's DMA here.
       if (more2) {
-        issue(m0, n0, t + 2, 3);
+        issue(u, voA, voB, t + 2, 3);
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!more1 && tnext < cend) {
-          prologue(m0n, n0n);
-          primed = true;
+          const Unit4 un = unit(tnext);
+          if (un.nt > 0) {
+            prologue(un);
+            primed = true;
+          }
         }
       }
       SEG_BARRIER();
@@ -536,12 +608,57 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args
     }
     if (nt == 0 && wm == 0) SEG_BARRIER();
     STAMP(2);
-    if (SPLIT) epilogue4_slab(args, acc, z, m0, n0, wm, wn, lane);
-    else epilogue4<OutT, EPI>(args, acc, z, m0, n0, wm, wn, lane);
+    if (GRP) {
+      const WgProb& q = gp->p[u.prob];
+      if (SPLIT) {
+        epilogue4_slab(gp->ws + q.slab_off + (int64_t)u.slice * q.N * q.K, q.N, q.K, 1.f, acc, m0, n0, wm, wn, lane);
+      } else {
+        maeclip_gemm_args ea = args;
+        ea.M = q.N;
+        ea.N = q.K;
+        ea.C = q.dw;
+        ea.ldc = q.K;
+        ea.alpha = 1.f;
+        ea.beta = gp->beta;
+        epilogue4<OutT, EPI>(ea, acc, 0, m0, n0, wm, wn, lane);
+      }
+    } else if (SPLIT) {
+      epilogue4_slab(args.workspace + ((int64_t)z * args.splitk + blockIdx.y) * args.M * args.N, (int)args.M,
+                     (int)args.N, args.alpha, acc, m0, n0, wm, wn, lane);
+    } else {
+      epilogue4<OutT, EPI>(args, acc, z, m0, n0, wm, wn, lane);
+    }
     STAMP(3);
 #ifdef GEMM4_STAMPS
     ++ntile;
 #endif
+  }
+}
+
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
+  gemm4_body<LA, LB, OutT, EPI, SPLIT, false>(args, nullptr);
+}
+
+// grouped weight gradients: RC x RC, fp32 out, no epilogue (beta only)
+template <bool SPLIT>
+__global__ void __launch_bounds__(512) wgrad4_kernel(const WgGroup grp) {
+  maeclip_gemm_args a = {};
+  a.alpha = 1.f;
+  gemm4_body<LAY_RC, LAY_RC, float, EPI_NONE, SPLIT, true>(a, &grp);
+}
+
+// S slabs of every problem -> dW (fixed summation order)
+__global__ void __launch_bounds__(256) wgrad4_reduce_kernel(const WgGroup grp) {
+  const WgProb& q = grp.p[blockIdx.y];
+  const int64_t NK = (int64_t)q.N * q.K;
+  const float* ws = grp.ws + q.slab_off;
+  for (int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; e < NK; e += (int64_t)gridDim.x * 1024) {
+    v4f v = *(const v4f*)(ws + e);
+    for (int s = 1; s < grp.S; ++s) v += *(const v4f*)(ws + s * NK + e);
+    float* d = q.dw + e;
+    if (grp.beta != 0.f) v += grp.beta * *(const v4f*)d;
+    *(v4f*)d = v;
   }
 }
 
@@ -619,3 +736,157 @@ int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
   return out4<LAY_RC, LAY_RC>(a, s);
 }
 }  // namespace maeclip
+
+// ------------------------------------------------- grouped weight gradients
+namespace {
+
+int wg_ncu() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+bool wg_v4_ok(const maeclip_wgrad_problem* pr, int n, int64_t M, int32_t dtype) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (dtype != MAECLIP_BF16 || M <= 0 || M % 64 != 0 || M >= (1ll << 31)) return false;
+  for (int i = 0; i < n; ++i) {
+    const maeclip_wgrad_problem& q = pr[i];
+    if (q.N < 256 || q.K < 256 || q.N % 8 || q.K % 8 || q.ldy % 8 || q.ldx % 8) return false;
+    if (q.ldy < q.N || q.ldx < q.K) return false;
+    if (!al16(q.dy) || !al16(q.x) || !al16(q.dw)) return false;
+    if (M * q.ldy * 2 >= 0x7fffffffLL || M * q.ldx * 2 >= 0x7fffffffLL) return false;
+  }
+  return true;
+}
+
+int wg_tiles(const maeclip_wgrad_problem& q) { return (int)(((q.N + 255) / 256) * ((q.K + 255) / 256)); }
+
+// Slices per tile for one launch of T tiles: the S minimising the number of
+// waves of units per tile-K, ceil(T*S/ncu)/S, with a 10% charge for the fp32
+// slab round trip of S > 1; every slice keeps >= 16 K-tiles. The encoder's 48
+// dW (1296 tiles) take S = 1, the decoder's 32 (384 tiles) S = 2.
+int wg_splits(int T, int64_t M) {
+  const int ncu = wg_ncu();
+  int best = 1;
+  double best_cost = (double)((T + ncu - 1) / ncu);
+  for (int S = 2; S <= 16; ++S) {
+    if (M / 64 / S < 16) break;
+    const double cost = (double)((T * S + ncu - 1) / ncu) / S * 1.1;
+    if (cost < best_cost - 1e-9) {
+      best = S;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+int64_t wg_chunk_ws(const maeclip_wgrad_problem* pr, int n, int64_t M) {
+  int T = 0;
+  int64_t nk = 0;
+  for (int i = 0; i < n; ++i) {
+    T += wg_tiles(pr[i]);
+    nk += pr[i].N * pr[i].K;
+  }
+  const int S = wg_splits(T, M);
+  return S > 1 ? (int64_t)S * nk * 4 : 0;
+}
+
+}  // namespace
+
+extern "C" int64_t maeclip_wgrad_grouped_workspace(const maeclip_wgrad_problem* probs, int32_t nprob, int64_t M,
+                                                   int32_t dtype) {
+  if (!probs || nprob <= 0 || !wg_v4_ok(probs, nprob, M, dtype)) return 0;
+  int64_t ws = 0;
+  for (int c = 0; c < nprob; c += WG_MAX) ws = std::max(ws, wg_chunk_ws(probs + c, std::min(WG_MAX, nprob - c), M));
+  return ws;
+}
+
+extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int32_t nprob, int64_t M, int32_t dtype,
+                                         float beta, void* workspace, int64_t ws_bytes, void* stream) {
+  MC_CHECK_ARG(probs != nullptr && nprob >= 0, "maeclip_wgrad_grouped: bad problem list");
+  MC_CHECK_ARG(M >= 0, "maeclip_wgrad_grouped: bad token count");
+  if (nprob == 0 || M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (!wg_v4_ok(probs, nprob, M, dtype)) {
+    // shapes / dtypes outside the grouped kernel: one maeclip_gemm per problem
+    for (int i = 0; i < nprob; ++i) {
+      const maeclip_wgrad_problem& q = probs[i];
+      maeclip_gemm_args a = {};
+      a.A = q.dy;
+      a.B = q.x;
+      a.C = q.dw;
+      a.M = q.N;
+      a.N = q.K;
+      a.K = M;
+      a.lda = q.ldy;
+      a.ldb = q.ldx;
+      a.ldc = q.K;
+      a.batch = 1;
+      a.dtype = dtype;
+      a.out_dtype = MAECLIP_F32;
+      a.a_layout = LAY_RC;
+      a.b_layout = LAY_RC;
+      a.alpha = 1.f;
+      a.beta = beta;
+      a.splitk = 1;
+      const int rc = maeclip_gemm(&a, stream);
+      if (rc != 0) return rc;
+    }
+    return 0;
+  }
+  MC_CHECK_ARG(ws_bytes >= maeclip_wgrad_grouped_workspace(probs, nprob, M, dtype) &&
+                   (ws_bytes == 0 || ((uintptr_t)workspace & 15) == 0),
+               "maeclip_wgrad_grouped: workspace too small or misaligned");
+  for (int c = 0; c < nprob; c += WG_MAX) {
+    const int n = std::min(WG_MAX, nprob - c);
+    WgGroup g = {};
+    g.np = n;
+    g.Mtok = (int)M;
+    g.beta = beta;
+    g.ws = (float*)workspace;
+    int T = 0;
+    int64_t so = 0;
+    for (int i = 0; i < n; ++i) {
+      const maeclip_wgrad_problem& q = probs[c + i];
+      WgProb& w = g.p[i];
+      w.dy = (const bf16_t*)q.dy;
+      w.x = (const bf16_t*)q.x;
+      w.dw = q.dw;
+      w.N = (int)q.N;
+      w.K = (int)q.K;
+      w.ldy = (int)q.ldy;
+      w.ldx = (int)q.ldx;
+      w.tile_begin = T;
+      T += wg_tiles(q);
+    }
+    g.T = T;
+    g.S = wg_splits(T, M);
+    if (g.S > 1) {
+      for (int i = 0; i < n; ++i) {
+        MC_CHECK_ARG(so < (1ll << 31), "maeclip_wgrad_grouped: workspace offsets exceed 2^31 floats");
+        g.p[i].slab_off = (int)so;
+        so += (int64_t)g.S * g.p[i].N * g.p[i].K;
+      }
+    }
+    const int units = T * g.S, grid = std::min(units, wg_ncu());
+    if (g.S > 1) {
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      hipLaunchKernelGGL(wgrad4_kernel<true>, dim3(grid), dim3(512), LDS_BYTES, s, g);
+      MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
+      int64_t maxnk = 0;
+      for (int i = 0; i < n; ++i) maxnk = std::max(maxnk, (int64_t)g.p[i].N * g.p[i].K);
+      const int gx = (int)std::min<int64_t>((maxnk / 4 + 255) / 256, 1024);
+      hipLaunchKernelGGL(wgrad4_reduce_kernel, dim3(gx, n), dim3(256), 0, s, g);
+      MC_CHECK_LAUNCH("maeclip_wgrad_grouped(reduce)");
+    } else {
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(grid), dim3(512), LDS_BYTES, s, g);
+      MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
+    }
+  }
+  return 0;
+}

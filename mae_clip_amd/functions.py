@@ -44,21 +44,33 @@ def side_stream(device) -> torch.cuda.Stream:
 
 
 class WgradQueue:
-    """Weight-gradient GEMMs of a backward pass on the side stream.
+    """Weight-gradient GEMMs of a transformer stack's backward.
 
-    Each dW = dy^T x only feeds the optimizer, so it runs beside the
-    dgrad -> LN -> attention chain of the current stream and fills the CUs that
-    chain leaves idle (the tails of its persistent GEMMs, the HBM-bound LN /
-    attention kernels). Inputs get record_stream() so the caching allocator
-    does not hand their memory to the current stream while the side stream may
-    still read it; join() makes the current stream wait for every queued dW.
+    grouped (default): every dW = dy^T x of the stack is queued and join()
+    computes them all in ONE maeclip_wgrad_grouped call on the current stream
+    -- one persistent launch whose tiles (4 x layers problems) fill the 256 CUs
+    without the fp32 split-K slab round trip that a single 768x3072 or
+    512x2048 dW needs to occupy the chip (its inputs stay alive until then).
+    Otherwise each dW runs as it becomes ready, on the side stream beside the
+    dgrad -> LN -> attention chain (side=True) or inline. Inputs used on the
+    side stream get record_stream() so the caching allocator does not hand
+    their memory to the current stream while the side stream may still read
+    it; join() makes the current stream wait for every queued dW.
     """
 
-    def __init__(self, device, enabled=True):
+    def __init__(self, device, enabled=True, grouped=True):
         self.main = torch.cuda.current_stream(device)
-        self.side = side_stream(device) if enabled else None
+        self.side = side_stream(device) if (enabled and not grouped) else None
+        self.grouped = grouped
+        self.items = []
 
     def wgrad(self, dy, x):
+        if self.grouped:
+            out = torch.empty((dy.shape[1], x.shape[1]), device=dy.device, dtype=torch.float32)
+            if self.items and self.items[0][0].shape[0] != dy.shape[0]:
+                self.flush()
+            self.items.append((dy, x, out))
+            return out
         if self.side is None:
             return K.linear_wgrad(dy, x)
         M, N = dy.shape
@@ -71,7 +83,13 @@ class WgradQueue:
         out.record_stream(self.side)
         return out
 
+    def flush(self):
+        if self.items:
+            K.wgrad_grouped(self.items)
+            self.items = []
+
     def join(self):
+        self.flush()
         if self.side is not None:
             self.main.wait_stream(self.side)
 
@@ -86,7 +104,8 @@ class StackSpec:
     eps: float
     dtype: torch.dtype              # compute dtype of GEMM operands / activations
     wT: list                        # per block: (qkv, proj, fc1, fc2) weights in `dtype`
-    side: bool = True               # weight gradients on the side stream
+    side: bool = True               # weight gradients on the side stream (when not grouped)
+    grouped_wgrad: bool = True      # one grouped launch for all weight gradients of the stack
 
 
 PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
@@ -133,7 +152,7 @@ class TransformerStackFn(torch.autograd.Function):
         params = ctx.params
         grads = [None] * len(params)
         rb = K.ReduceBatch()
-        wq = WgradQueue(gy.device, spec.side)
+        wq = WgradQueue(gy.device, spec.side, spec.grouped_wgrad)
         g = gy.reshape(M, D)
         if not g.is_contiguous():
             g = g.contiguous()
@@ -302,7 +321,8 @@ class MaeHeadSpec:
     mask_count: float
     loss_scale: float
     dtype: torch.dtype
-    w_T: torch.Tensor        # decoder_pred weight in dtype
+    w_T: torch.Tensor        # decoder_pred weight in dtype, [Npad, Dd] (zero rows past p*p*C)
+    b_pad: torch.Tensor = None   # decoder_pred bias padded to Npad (None: no padding)
 
 
 class MaeHeadLossFn(torch.autograd.Function):
@@ -311,13 +331,14 @@ class MaeHeadLossFn(torch.autograd.Function):
         B, n, Dd = xd.shape
         x2 = xd.view(B * n, Dd)
         h, m, r, _, _ = K.ln_fwd(x2, dn_w, dn_b, 1e-6, out_dtype=spec.dtype)
-        pred = K.linear_fwd(h, spec.w_T, bp)
+        pred = K.linear_fwd(h, spec.w_T, bp if spec.b_pad is None else spec.b_pad)
         row = K.mae_loss_fwd(pred, img, mask, spec.p, spec.norm_pix)
         loss = K.colsum_reduce(row.view(-1, 1), scale=1.0 / spec.mask_count).view(())
         ctx.save = (x2, h, m, r, pred, img, mask)
         ctx.spec = spec
         ctx.dn_w = dn_w
         ctx.shape = xd.shape
+        ctx.P = wp.shape[0]
         return loss
 
     @staticmethod
@@ -328,6 +349,8 @@ class MaeHeadLossFn(torch.autograd.Function):
                                    spec.loss_scale)
         dh = K.linear_dgrad(dpred, spec.w_T)
         dWp = K.linear_wgrad(dpred, h)
+        if dWp.shape[0] != ctx.P:
+            dWp = dWp[:ctx.P].contiguous()
         dbp = _reduce(cs)
         dx, _, pg, pb, _ = K.ln_bwd(dh, x2, m, r, ctx.dn_w)
         return dx.view(ctx.shape), None, None, None, _reduce(pg), _reduce(pb), dWp, dbp

@@ -112,6 +112,32 @@ def linear_wgrad(dy, x, out=None, beta=0.0, bias_grad_out=None):
     return out
 
 
+def wgrad_grouped(items, beta=0.0):
+    """dW_p = dy_p^T x_p for a list of (dy [M, N_p], x [M, K_p], out [N_p, K_p] f32)
+    sharing the token count M, in one maeclip_wgrad_grouped call (one persistent
+    launch per 48 problems on the bf16 path)."""
+    if not items:
+        return
+    M = items[0][0].shape[0]
+    n = len(items)
+    probs = (L.WgradProblem * n)()
+    for i, (dy, x, out) in enumerate(items):
+        _dev(dy, x, out)
+        if dy.shape[0] != M or x.shape[0] != M or dy.dtype != x.dtype or out.dtype != torch.float32:
+            raise ValueError("wgrad_grouped: problems must share the token count and dtype (fp32 dW)")
+        if out.shape != (dy.shape[1], x.shape[1]) or out.stride(0) != x.shape[1] or dy.stride(1) != 1 \
+                or x.stride(1) != 1:
+            raise ValueError("wgrad_grouped: dW must be dense [N, K]; dy/x row-major")
+        q = probs[i]
+        q.dy, q.x, q.dw = dy.data_ptr(), x.data_ptr(), out.data_ptr()
+        q.N, q.K, q.ldy, q.ldx = dy.shape[1], x.shape[1], dy.stride(0), x.stride(0)
+    dt = _dt(items[0][0])
+    lib = L.lib()
+    nb = int(lib.maeclip_wgrad_grouped_workspace(probs, n, M, dt))
+    ws = torch.empty((max(nb, 4) // 4,), device=items[0][0].device, dtype=torch.float32) if nb > 0 else None
+    _call("maeclip_wgrad_grouped", probs, n, M, dt, beta, _ptr(ws), nb, _stream())
+
+
 # ------------------------------------------------------------- reductions
 def colsum_reduce(partial, out=None, accumulate=False, scale=1.0):
     _dev(partial)
@@ -317,7 +343,9 @@ def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=
     B, Cc, S, _ = img.shape
     L_ = mask.shape[1]
     P = Cc * p * p
-    dpred = torch.empty_like(pred)
+    # padded pred rows (decoder_pred N rounded up for the GEMM): the pad columns
+    # of dpred must be zeros (they meet the zero rows of the padded weight)
+    dpred = torch.empty_like(pred) if pred.shape[1] == P else torch.zeros_like(pred)
     cs = torch.empty((B, P), device=img.device, dtype=torch.float32)
     a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
                       row_loss=None, dpred=dpred.data_ptr(), lddp=dpred.stride(0), grad_out=_ptr(grad_out),

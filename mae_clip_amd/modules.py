@@ -141,7 +141,7 @@ def run_stack(blocks, x, heads, dtype, cache: WeightCache):
     B, n, D = x.shape
     wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in blocks]
     spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=blocks[0].norm1.eps, dtype=dtype, wT=wT,
-                        side=bool(CFG.side_stream))
+                        side=bool(CFG.side_stream), grouped_wgrad=bool(CFG.wgrad_grouped))
     params = [p for blk in blocks for p in blk.stack_params()]
     return Fn.TransformerStackFn.apply(x, spec, *params)
 
@@ -202,10 +202,19 @@ class VisionTransformer(nn.Module):
         w = pe.proj.weight
         kreal = w[0].numel()
         epc = 8 if dtype == torch.bfloat16 else 4
-        if kreal % epc:
-            raise NotImplementedError("patch-embed K must be a multiple of 8 (bf16) / 4 (fp32)")
-        spec = Fn.PatchSpec(B=B, L=L, keep=keep, p=pe.patch_size, kpad=kreal, dtype=dtype,
-                            w_T=cache.get(w, dtype, (self.embed_dim, kreal)))
+        w_T, kpad = cache.get(w, dtype, (self.embed_dim, kreal)), kreal
+        if kreal % epc or (dtype == torch.bfloat16 and kreal % 64):
+            # p*p*3 = 588 at patch 14: the patch rows are gathered with zero
+            # columns up to a multiple of 64 (16-B rows, the v4 GEMM's K step)
+            # and the weight shadow is padded to match (dW is sliced back)
+            kpad = (kreal + 63) // 64 * 64
+            buf = getattr(self, "_w_pad", None)
+            if buf is None or buf.shape != (self.embed_dim, kpad) or buf.dtype != dtype or buf.device != w.device:
+                buf = torch.zeros((self.embed_dim, kpad), device=w.device, dtype=dtype)
+                self._w_pad = buf
+            buf[:, :kreal].copy_(w_T)
+            w_T = buf
+        spec = Fn.PatchSpec(B=B, L=L, keep=keep, p=pe.patch_size, kpad=kpad, dtype=dtype, w_T=w_T)
         x = Fn.PatchTokensFn.apply(img, ids_shuffle, ids_restore, spec, w, pe.proj.bias, self.cls_token,
                                    self.pos_embed)
         return run_stack(self.blocks, x, self.num_heads, dtype, cache)
@@ -453,6 +462,21 @@ class MAEDecoder(nn.Module):
         nn.init.zeros_(self.decoder_embed.bias)
         _trunc_normal_(self.decoder_pred.weight)
         nn.init.zeros_(self.decoder_pred.bias)
+        self._pred_pad = None
+
+    def padded_pred(self, w_T):
+        """decoder_pred weight shadow / bias copied into buffers whose output rows
+        are rounded up to a multiple of 64 (pad rows / entries stay zero)."""
+        P, Dd = w_T.shape
+        npad = (P + 63) // 64 * 64
+        pad = self._pred_pad
+        if pad is None or pad[0].shape != (npad, Dd) or pad[0].dtype != w_T.dtype or pad[0].device != w_T.device:
+            pad = (torch.zeros((npad, Dd), device=w_T.device, dtype=w_T.dtype),
+                   torch.zeros((npad,), device=w_T.device, dtype=torch.float32))
+            self._pred_pad = pad
+        pad[0][:P].copy_(w_T)
+        pad[1][:P].copy_(self.decoder_pred.bias.detach())
+        return pad
         for blk in self.decoder_layers:
             blk.init_weights()
 

@@ -218,6 +218,48 @@ def test_wgrad_splitk_v4(dev, mnk):
     assert torch.equal(dW, dW2)
 
 
+@pytest.mark.parametrize("case", ["encoder4", "decoder2x4", "few_tiles_splitk", "strided", "fp32_fallback"])
+def test_wgrad_grouped(dev, case):
+    """maeclip_wgrad_grouped: the 4 weight gradients of transformer blocks
+    (qkv, proj, fc1, fc2) in one launch vs fp64 torch; S = 1 and split-K
+    groups, strided dy (a column slice), beta accumulation, the per-problem
+    fallback for fp32 -- bit-identical across repeated runs (deterministic)."""
+    from mae_clip_amd import _lib
+    dt = torch.float32 if case == "fp32_fallback" else torch.bfloat16
+    if case in ("encoder4", "strided", "fp32_fallback"):
+        M, shapes = 3200, [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
+    elif case == "decoder2x4":
+        M, shapes = 6400, [(1536, 512), (512, 512), (2048, 512), (512, 2048)] * 2
+    else:
+        M, shapes = 4096, [(512, 256), (256, 512)]   # 4 tiles -> split-K slices
+    items, refs = [], []
+    for i, (N, Kd) in enumerate(shapes):
+        if case == "strided":
+            dy = _rand((M, N + 64), dt, dev, seed=60 + i)[:, 32:32 + N]
+        else:
+            dy = _rand((M, N), dt, dev, seed=60 + i)
+        x = _rand((M, Kd), dt, dev, seed=80 + i)
+        out = torch.empty((N, Kd), device=dev, dtype=torch.float32)
+        items.append((dy, x, out))
+        refs.append(_ref_mm(dy.t(), x))
+    if case == "few_tiles_splitk":
+        probs = (_lib.WgradProblem * 2)()
+        for q, (dy, x, out) in zip(probs, items):
+            q.dy, q.x, q.dw, q.N, q.K, q.ldy, q.ldx = dy.data_ptr(), x.data_ptr(), out.data_ptr(), dy.shape[1], \
+                x.shape[1], dy.stride(0), x.stride(0)
+        assert _lib.lib().maeclip_wgrad_grouped_workspace(probs, 2, M, 1) > 0
+    K.wgrad_grouped(items)
+    for (dy, x, out), ref in zip(items, refs):
+        assert (out.double() - ref).abs().max().item() / ref.abs().max().item() < 1e-5
+    first = [o.clone() for _, _, o in items]
+    K.wgrad_grouped(items)
+    for (_, _, out), f in zip(items, first):
+        assert torch.equal(out, f)
+    K.wgrad_grouped(items, beta=1.0)      # dW += dy^T x
+    for (dy, x, out), ref in zip(items, refs):
+        assert (out.double() - 2 * ref).abs().max().item() / ref.abs().max().item() < 1e-5
+
+
 def test_colsum_two_pass(dev):
     part = _rand((1000, 768), torch.float32, dev, seed=43)
     out = K.colsum_reduce(part)

@@ -80,6 +80,31 @@ def test_vitb_shapes_bf16_step(dev):
             assert p.grad is not None and torch.isfinite(p.grad).all().item(), n_
 
 
+def test_vitl14_336_shapes_bf16_vs_oracle(dev):
+    """C4 shapes (ViT-L/14 @336: 576 patches of 588 = 14*14*3 values, 145 visible
+    tokens, D 1024 / 16 heads; decoder n = 577, hd 32 -- K/V/Q/dO of one head
+    just fit the 160 KiB LDS in the bf16 backward) with the encoder cut to 4
+    blocks and B = 4 so the fp64 CPU oracle stays fast: bf16 production loss vs
+    the oracle on the same weights (rel 2e-2, bf16 operands) and finite grads.
+    Patch-embed K = 588 is not a multiple of 64: it takes the GEMM fallback
+    below the v4 kernel. (The fp32 parity mode keeps [n][HD] fp32 images in
+    LDS and is limited to n <= 256 at HD 32.)"""
+    prod, ref = build_pair("bf16", model_name="vit_large_patch14_336", size=336, image_embedding=1024,
+                           text_layers=2, mask_ratio=0.75, decoder_embed_dim=512, decoder_depth=2,
+                           decoder_num_heads=16, vit_depth=4)
+    prod.eval()
+    ref.eval()
+    batch = make_batch(4, 336)
+    loss = prod({k: v.to(dev) for k, v in batch.items()})
+    loss.backward()
+    for n_, p in prod.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None and torch.isfinite(p.grad).all().item(), n_
+    with torch.no_grad():
+        rloss = ref(dict(batch, image=batch["image"].double())).item()
+    assert abs(loss.item() - rloss) < 2e-2 * max(1.0, abs(rloss)), (loss.item(), rloss)
+
+
 def test_vitb_bf16_grads_match_fp32(dev):
     """Every trainable gradient of the bf16 production path at ViT-B shapes whose
     GEMMs take the v4 kernel (token counts % 64 == 0, split-K wgrad) vs the fp32

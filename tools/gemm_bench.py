@@ -41,19 +41,48 @@ def time_fn(fn, reps=20):
     return s.elapsed_time(e) / reps / 1e3
 
 
+if os.environ.get("GEMM_SET") == "epi":   # production epilogues (functions.py), no hipBLASLt leg
+    SHAPES = [("dec fc2 dgrad*gelu'", D, 2048, 512, 0, 1, 5), ("enc fc2 dgrad*gelu'", E, 3072, 768, 0, 1, 5),
+              ("dec fc1 fwd gelu", D, 2048, 512, 0, 0, 4), ("enc fc1 fwd gelu", E, 3072, 768, 0, 0, 4),
+              ("dec fc2 fwd +res", D, 512, 2048, 0, 0, 2), ("enc fc2 fwd +res", E, 768, 3072, 0, 0, 2),
+              ("dec proj fwd +res", D, 512, 512, 0, 0, 2), ("enc proj fwd +res", E, 768, 768, 0, 0, 2),
+              ("dec proj dgrad", D, 512, 512, 0, 1, 0), ("enc proj dgrad", E, 768, 768, 0, 1, 0),
+              ("dec qkv dgrad", D, 512, 1536, 0, 1, 0), ("enc qkv dgrad", E, 768, 2304, 0, 1, 0)]
+
+
+def epi_kwargs(epi, M, N):
+    if epi == K.EPI_RESID:
+        return dict(resid=torch.randn(M, N, device=dev), ldr=N)
+    if epi in (K.EPI_GELU, K.EPI_GELU_D):
+        return dict(aux_out=torch.empty(M, N, device=dev, dtype=torch.bfloat16), ldaux=N,
+                    bias=torch.randn(N, device=dev))
+    if epi in (K.EPI_MUL_AUX, K.EPI_DGELU):
+        return dict(aux=torch.rand(M, N, device=dev).to(torch.bfloat16), ldaux=N)
+    return {}
+
+
 res = []
-for name, M, N, Kd, la, lb in SHAPES:
+for shp in SHAPES:
+    name, M, N, Kd, la, lb = shp[:6]
+    epi = shp[6] if len(shp) > 6 else -1
     A = mk(M, Kd) if la == 0 else mk(Kd, M)
     B = mk(N, Kd) if lb == 0 else mk(Kd, N)
-    C = torch.empty(M, N, device=dev, dtype=torch.float32 if (la, lb) == (1, 1) else torch.bfloat16)
+    C = torch.empty(M, N, device=dev, dtype=torch.float32 if (la, lb) == (1, 1) or epi == 2 else torch.bfloat16)
     S = 1
     ws = None
     if (la, lb) == (1, 1):  # production wgrad path: deterministic split-K
         from mae_clip_amd import _lib
         S = int(_lib.lib().maeclip_gemm_splitk(M, N, Kd))
         ws = torch.empty(S * M * N, device=dev) if S > 1 else None
-    f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, la, lb, splitk=S, workspace=ws)
+    kw = epi_kwargs(epi, M, N) if epi >= 0 else {}
+    f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, la, lb, splitk=S, workspace=ws,
+                       epilogue=max(epi, 0), **kw)
     t = time_fn(f)
+    if epi >= 0:
+        fl = 2.0 * M * N * Kd
+        r = dict(name=name, M=M, N=N, K=Kd, epi=epi, ours_tflops=round(fl / t / 1e12, 1), ours_us=round(t * 1e6, 1))
+        print(json.dumps(r), flush=True)
+        continue
     At = A if la == 0 else A.t()
     Bt = B.t() if lb == 0 else B
     tt = time_fn(lambda: torch.matmul(At, Bt))
