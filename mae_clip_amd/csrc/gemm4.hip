@@ -766,17 +766,20 @@ bool wg_v4_ok(const maeclip_wgrad_problem* pr, int n, int64_t M, int32_t dtype) 
 int wg_tiles(const maeclip_wgrad_problem& q) { return (int)(((q.N + 255) / 256) * ((q.K + 255) / 256)); }
 
 // Slices per tile for one launch of T tiles: the S minimising the number of
-// waves of units per tile-K, ceil(T*S/ncu)/S, with a 10% charge for the fp32
-// slab round trip of S > 1; every slice keeps >= 16 K-tiles. The encoder's 48
-// dW (1296 tiles) take S = 1, the decoder's 32 (384 tiles) S = 2.
+// waves of units per tile-K, ceil(T*S/ncu)/S, where S > 1 must beat S = 1 by
+// 15% to pay for the fp32 slab write + reduce, and S <= 4 (the slab traffic
+// grows with S while the wave quantisation it fixes does not); every slice
+// keeps >= 16 K-tiles. The encoder's 48 dW (1296 tiles: 5.06 waves) take S = 1, the
+// decoder's 32 (384 tiles: 1.5 waves) S = 2.
 int wg_splits(int T, int64_t M) {
   const int ncu = wg_ncu();
+  const double c1 = (double)((T + ncu - 1) / ncu);
   int best = 1;
-  double best_cost = (double)((T + ncu - 1) / ncu);
-  for (int S = 2; S <= 16; ++S) {
+  double best_cost = c1;
+  for (int S = 2; S <= 4; ++S) {
     if (M / 64 / S < 16) break;
-    const double cost = (double)((T * S + ncu - 1) / ncu) / S * 1.1;
-    if (cost < best_cost - 1e-9) {
+    const double cost = (double)((T * S + ncu - 1) / ncu) / S;
+    if (cost < 0.85 * c1 && cost < best_cost - 1e-9) {
       best = S;
       best_cost = cost;
     }
