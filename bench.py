@@ -208,17 +208,27 @@ def main():
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one HIP graph per step")
     ap.add_argument("--gemm-table", action="store_true", help="per-shape GEMM times to stderr")
+    ap.add_argument("--dp", action="store_true",
+                    help="data-parallel code path (RCCL process group, gathers, grad all-reduce) even at N=1")
     ap.add_argument("--no-side-stream", action="store_true",
                     help="text tower and weight gradients on the main stream (config.side_stream = False)")
     args = ap.parse_args()
+    # the driver reads ONE JSON line from stdout: route everything else written
+    # to fd 1 (RCCL's version banner, library chatter) to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    use_dp = world > 1 or args.dp
+    if use_dp:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
 
     from mae_clip_amd import kernels as K
     from mae_clip_amd.optim import AdamW
@@ -230,7 +240,7 @@ def main():
                              decoder_num_heads=16, precision="bf16",
                              side_stream=not args.no_side_stream)).to(device)
     model.train()
-    dp = DataParallel(model) if world > 1 else None
+    dp = DataParallel(model) if use_dp else None
     opt = AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
     batch = synthetic_batch(args.batch, 224, 25, 1000 + rank, device)
 
@@ -240,7 +250,7 @@ def main():
 
     # one HIP graph per step (mae_clip_amd.graph): step 1 eager, step 2 captured,
     # then replays. Data-parallel runs and --gemm-table stay eager.
-    use_graph = world == 1 and not args.no_graph and not args.gemm_table
+    use_graph = not use_dp and not args.no_graph and not args.gemm_table
     runner = CapturedStep(model, opt, enabled=use_graph, eager_steps=2)
     warmup = max(args.warmup, 3) if use_graph else max(args.warmup, 2)
 
@@ -269,7 +279,7 @@ def main():
             timer.records = {}
     torch.cuda.synchronize()
     timer.records = {}
-    if world > 1:
+    if use_dp:
         dist.barrier()
     torch.cuda.synchronize()
     timer.active = True
@@ -281,7 +291,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timer.active = False
-    if world > 1:
+    if use_dp:
         dist.barrier()
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,8 +334,9 @@ def main():
                 out["loss_delta_vs_ref"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if use_dp:
         dist.destroy_process_group()
 
 

@@ -105,8 +105,8 @@ class DataParallel:
         for i, w in self._works:
             w.wait()
             grads = [p.grad for p in self.buckets[i]]
-            for g, s in zip(grads, torch._utils._unflatten_dense_tensors(self._flats[i], grads)):
-                g.copy_(s)
+            # one multi-tensor copy per bucket (not one launch per parameter)
+            torch._foreach_copy_(grads, torch._utils._unflatten_dense_tensors(self._flats[i], grads))
         self._works = []
         self._flats = [None] * len(self.buckets)
         self._pending = [0] * len(self.buckets)

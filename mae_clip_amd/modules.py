@@ -137,13 +137,23 @@ class Block(nn.Module):
             nn.init.zeros_(lin.bias)
 
 
-def run_stack(blocks, x, heads, dtype, cache: WeightCache):
+def run_stack(blocks, x, heads, dtype, cache: WeightCache, chunk=None):
+    """The blocks as one TransformerStackFn, or as consecutive Functions of
+    `chunk` blocks: autograd accumulates a Function's parameter gradients when
+    its backward returns, so under data parallelism a chunked encoder hands its
+    upper blocks' gradients to the bucketed all-reduce while the backward of the
+    lower blocks is still running (the all-reduce of the last stack in the
+    backward is otherwise fully exposed)."""
     B, n, D = x.shape
-    wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in blocks]
-    spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=blocks[0].norm1.eps, dtype=dtype, wT=wT,
-                        side=bool(CFG.side_stream), grouped_wgrad=bool(CFG.wgrad_grouped))
-    params = [p for blk in blocks for p in blk.stack_params()]
-    return Fn.TransformerStackFn.apply(x, spec, *params)
+    chunk = chunk or len(blocks)
+    for c0 in range(0, len(blocks), chunk):
+        part = blocks[c0:c0 + chunk]
+        wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in part]
+        spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=part[0].norm1.eps, dtype=dtype, wT=wT,
+                            side=bool(CFG.side_stream), grouped_wgrad=bool(CFG.wgrad_grouped))
+        params = [p for blk in part for p in blk.stack_params()]
+        x = Fn.TransformerStackFn.apply(x, spec, *params)
+    return x
 
 
 class PatchEmbed(nn.Module):
@@ -217,7 +227,11 @@ class VisionTransformer(nn.Module):
         spec = Fn.PatchSpec(B=B, L=L, keep=keep, p=pe.patch_size, kpad=kpad, dtype=dtype, w_T=w_T)
         x = Fn.PatchTokensFn.apply(img, ids_shuffle, ids_restore, spec, w, pe.proj.bias, self.cls_token,
                                    self.pos_embed)
-        return run_stack(self.blocks, x, self.num_heads, dtype, cache)
+        chunk = None
+        if torch.distributed.is_available() and torch.distributed.is_initialized() and \
+                torch.distributed.get_world_size() > 1:
+            chunk = CFG.dp_encoder_chunk or None
+        return run_stack(self.blocks, x, self.num_heads, dtype, cache, chunk=chunk)
 
     def forward(self, img):
         """timm semantics: pooled + fc_norm features [B, D] (no masking)."""

@@ -190,3 +190,36 @@ def test_captured_step_matches_eager(dev, precision):
     st_e = [s["step"] for s in oe.state.values()]
     st_g = [s["step"] for s in og.state.values()]
     assert st_e == st_g and set(st_e) == {5}
+
+
+def test_chunked_stack_matches_whole(dev):
+    """run_stack(chunk=k) (the data-parallel encoder split into consecutive
+    autograd Functions so gradients reach the all-reduce early) matches one
+    Function over all blocks: activations and input grads bit-identical;
+    parameter grads within bf16 rounding (a chunk's top fc2 bias gradient is
+    column-summed from the incoming fp32 gradient instead of from the LN
+    backward's partials of its bf16 copy, and a small group's dW may take
+    split-K slices)."""
+    from mae_clip_amd import modules as Mo
+    torch.manual_seed(0)
+    blocks = torch.nn.ModuleList([Mo.Block(768, 12) for _ in range(4)]).to(dev)
+    for b in blocks:
+        b.init_weights()
+    cache = Mo.WeightCache()
+    for b in blocks:
+        for p in b.gemm_weights():
+            cache.register(p, p.shape)
+    cache.refresh(torch.bfloat16)
+    x0 = torch.randn(64, 50, 768, device=dev)
+    outs = []
+    for chunk in (None, 2, 1):
+        for p in blocks.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_()
+        y = Mo.run_stack(blocks, x, 12, torch.bfloat16, cache, chunk=chunk)
+        (y * torch.linspace(-1, 1, y.numel(), device=dev).view_as(y)).sum().backward()
+        outs.append((y.detach(), x.grad, [p.grad.clone() for p in blocks.parameters()]))
+    for i, (y, gx, gp) in enumerate(outs[1:]):
+        assert torch.equal(y, outs[0][0]) and torch.equal(gx, outs[0][1])
+        for a, b in zip(gp, outs[0][2]):
+            assert torch.allclose(a, b, rtol=1e-3, atol=1e-4 * b.abs().max().item())
