@@ -95,8 +95,9 @@ int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K);
  *   dw_p[n][k] = sum_m dy_p[m*ldy + n] * x_p[m*ldx + k]  (+ beta * dw_p[n][k])
  * for p < nprob, m < M (tokens, shared by every problem). dw is fp32 dense
  * [N][K]; dy/x have `dtype`. bf16 problems with M % 64 == 0 and N, K >= 256
- * share one persistent launch per 48 problems (no split-K slab unless the tile
- * count leaves > 20% of the CUs idle); others run one maeclip_gemm each.
+ * share one persistent launch per 48 problems (split-K slabs, S <= 4, only when
+ * they cut the waves of output tiles by >= 15%); others run one maeclip_gemm
+ * each.
  * Deterministic (fixed summation order). workspace: >= the bytes
  * maeclip_wgrad_grouped_workspace() returns (0 is common), 16-B aligned. */
 typedef struct {
@@ -275,6 +276,31 @@ typedef struct {
   int32_t B, C, S, p, keep, dtype;
 } maeclip_patch_args;
 int32_t maeclip_patch_gather(const maeclip_patch_args* args, void* stream);
+
+/* Input pipeline. Replaces dataset.py:44-58 on the host: albumentations
+ * Normalize(mean, std, max_pixel_value) of the decoded RGB uint8 HWC image
+ * (dataset.py:49) and permute(2, 0, 1).float() (dataset.py:34), for a batch:
+ * src uint8 [B][H][W][3] dense -> dst fp32 [B][3][H][W] dense,
+ * dst = (float(src) - mean*max_pixel) * (1 / (std*max_pixel)) in fp32. */
+typedef struct {
+  const uint8_t* src;
+  float* dst;
+  int64_t B, H, W;
+  float mean[3], std[3];
+  float max_pixel;
+} maeclip_image_u8_args;
+int32_t maeclip_image_normalize_u8(const maeclip_image_u8_args* args, void* stream);
+
+/* Retrieval (inference.py:40-45). l2_normalize replaces F.normalize(x, p=2,
+ * dim=-1): y = x / max(||x||_2, eps), fp32 [M][P] rows (strides ldx / ldy).
+ * topk_rows replaces torch.topk(dot_similarity, k) row-wise: s fp32 [Q][N]
+ * (row stride lds) -> vals [Q][k] descending, idx [Q][k] (int64), ties broken
+ * by the lower index; 1 <= k <= min(N, 1024). The similarity itself is an
+ * fp32 maeclip_gemm (text_n @ image_n^T). */
+int32_t maeclip_l2_normalize(const float* x, float* y, int64_t M, int64_t P, int64_t ldx, int64_t ldy, float eps,
+                             void* stream);
+int32_t maeclip_topk_rows(const float* s, int64_t Q, int64_t N, int64_t lds, int32_t k, float* vals, int64_t* idx,
+                          void* stream);
 
 /* timm _pos_embed on the visible tokens: x[b,0] = cls + pos[0];
  * x[b,1+j] = y[b*keep+j] + pos[1+ids_shuffle[b,j]]; bwd: dy rows, dpos, dcls. */

@@ -111,6 +111,11 @@ class WgradProblem(C.Structure):
     _fields_ = [("dy", c_vp), ("x", c_vp), ("dw", c_vp), ("N", c_i64), ("K", c_i64), ("ldy", c_i64), ("ldx", c_i64)]
 
 
+class ImageU8Args(C.Structure):
+    _fields_ = [("src", c_vp), ("dst", c_vp), ("B", c_i64), ("H", c_i64), ("W", c_i64),
+                ("mean", c_f32 * 3), ("std", c_f32 * 3), ("max_pixel", c_f32)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "maeclip_abi_version": (c_i32, []),
@@ -122,6 +127,9 @@ _SIGS = {
     "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
     "maeclip_wgrad_grouped_workspace": (c_i64, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32]),
     "maeclip_wgrad_grouped": (c_i32, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32, c_f32, c_vp, c_i64, c_vp]),
+    "maeclip_image_normalize_u8": (c_i32, [C.POINTER(ImageU8Args), c_vp]),
+    "maeclip_l2_normalize": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
+    "maeclip_topk_rows": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "maeclip_attn_fwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_attn_bwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_ln_fwd": (c_i32, [C.POINTER(LnFwdArgs), c_vp]),

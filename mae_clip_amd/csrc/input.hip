@@ -1,0 +1,87 @@
+// Input pipeline on the device.
+//
+// Replaces the per-image host transform of dataset.py:44-58: the decoded RGB
+// uint8 HWC image (cv2.imread + cvtColor, dataset.py:30-33) goes through
+// albumentations Normalize(max_pixel_value=255) (dataset.py:49) and
+// torch.tensor(image).permute(2, 0, 1).float() (dataset.py:34). The batch is
+// uploaded as uint8 (a quarter of the fp32 bytes over PCIe) and normalised
+// here, in HBM, straight into the model's NCHW fp32 input.
+//
+// Arithmetic is albumentations' normalize(): mean32 = f32(mean) * max_pixel,
+// den32 = 1 / (f32(std) * max_pixel) (both fp32, computed on the host with
+// IEEE division), out = (f32(x) - mean32) * den32 -- two roundings, no FMA.
+// HBM-bound: 3 B read + 12 B written per pixel.
+#include "common.h"
+#include "../../include/maeclip.h"
+
+namespace {
+constexpr int NTH = 256;
+
+struct NormConst {
+  float m[3], d[3];
+};
+
+// 4 consecutive pixels of one row per thread: three 4-B loads of interleaved
+// RGB, one 16-B store per plane (W % 4 == 0)
+__global__ void __launch_bounds__(NTH) normalize_u8_x4_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
+                                                               int64_t npix4, int64_t HW, NormConst k) {
+  const int64_t q = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  if (q >= npix4) return;
+  const int64_t pix = q * 4;              // global pixel index b*HW + y*W + x
+  const int64_t b = pix / HW, off = pix % HW;
+  const uint32_t* s = (const uint32_t*)(src + pix * 3);
+  const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];
+  const uint8_t v[12] = {(uint8_t)w0, (uint8_t)(w0 >> 8), (uint8_t)(w0 >> 16), (uint8_t)(w0 >> 24),
+                         (uint8_t)w1, (uint8_t)(w1 >> 8), (uint8_t)(w1 >> 16), (uint8_t)(w1 >> 24),
+                         (uint8_t)w2, (uint8_t)(w2 >> 8), (uint8_t)(w2 >> 16), (uint8_t)(w2 >> 24)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    v4f o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = (float)v[3 * j + c] - k.m[c];
+      o[j] = __fmul_rn(x, k.d[c]);
+    }
+    *(v4f*)(dst + (b * 3 + c) * HW + off) = o;
+  }
+}
+
+__global__ void __launch_bounds__(NTH) normalize_u8_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
+                                                            int64_t npix, int64_t HW, NormConst k) {
+  const int64_t pix = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  if (pix >= npix) return;
+  const int64_t b = pix / HW, off = pix % HW;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float x = (float)src[pix * 3 + c] - k.m[c];
+    dst[(b * 3 + c) * HW + off] = __fmul_rn(x, k.d[c]);
+  }
+}
+}  // namespace
+
+extern "C" int32_t maeclip_image_normalize_u8(const maeclip_image_u8_args* a, void* stream) {
+  MC_CHECK_ARG(a && a->src && a->dst, "maeclip_image_normalize_u8: null pointer");
+  MC_CHECK_ARG(a->B >= 0 && a->H > 0 && a->W > 0, "maeclip_image_normalize_u8: bad sizes");
+  MC_CHECK_ARG(a->max_pixel > 0.f, "maeclip_image_normalize_u8: max_pixel must be > 0");
+  NormConst k;
+  for (int c = 0; c < 3; ++c) {
+    MC_CHECK_ARG(a->std[c] > 0.f, "maeclip_image_normalize_u8: std must be > 0");
+    k.m[c] = a->mean[c] * a->max_pixel;
+    const volatile float sd = a->std[c] * a->max_pixel;   // fp32 product, then IEEE fp32 reciprocal
+    k.d[c] = 1.0f / sd;
+  }
+  const int64_t HW = a->H * a->W, npix = a->B * HW;
+  if (npix == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = a->W % 4 == 0 && ((uintptr_t)a->src & 3) == 0 && ((uintptr_t)a->dst & 15) == 0;
+  if (vec) {
+    const int64_t n4 = npix / 4;
+    hipLaunchKernelGGL(normalize_u8_x4_kernel, dim3((unsigned)((n4 + NTH - 1) / NTH)), dim3(NTH), 0, s, a->src, a->dst,
+                       n4, HW, k);
+  } else {
+    hipLaunchKernelGGL(normalize_u8_kernel, dim3((unsigned)((npix + NTH - 1) / NTH)), dim3(NTH), 0, s, a->src, a->dst,
+                       npix, HW, k);
+  }
+  MC_CHECK_LAUNCH("maeclip_image_normalize_u8");
+  return 0;
+}

@@ -1,0 +1,50 @@
+"""Device-side input pipeline.
+
+The reference's CLIPDataset.__getitem__ (dataset.py:24-37) decodes each image
+with cv2 (BGR -> RGB), runs albumentations Resize + Normalize
+(get_transforms, dataset.py:44-58) and permutes HWC -> CHW float32 on the host;
+main.py:55 then copies the fp32 batch to the GPU. Here decoding and resizing
+stay on the host (cv2 / PIL, unchanged), the batch crosses PCIe as uint8 HWC
+(4x fewer bytes) and libmaeclip normalises + transposes it in HBM
+(maeclip_image_normalize_u8), producing exactly the tensor the model takes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from .kernels import _dev, _call, _stream
+
+# ImageNet statistics of albumentations' A.Normalize defaults (dataset.py:49)
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def normalize_u8(images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, max_pixel_value=255.0,
+                 out: torch.Tensor = None) -> torch.Tensor:
+    """uint8 [B, H, W, 3] (RGB, HWC) on the device -> float32 [B, 3, H, W]:
+    (x - mean * max_pixel_value) / (std * max_pixel_value), albumentations'
+    normalize() arithmetic in fp32 (dataset.py:49, 34)."""
+    _dev(images, out)
+    if images.dtype != torch.uint8 or images.dim() != 4 or images.shape[-1] != 3:
+        raise ValueError(f"normalize_u8: expected uint8 [B, H, W, 3], got {images.dtype} {tuple(images.shape)}")
+    images = images.contiguous()
+    B, H, W, _ = images.shape
+    if out is None:
+        out = torch.empty((B, 3, H, W), device=images.device, dtype=torch.float32)
+    elif out.shape != (B, 3, H, W) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("normalize_u8: out must be a dense float32 [B, 3, H, W]")
+    a = L.ImageU8Args(src=images.data_ptr(), dst=out.data_ptr(), B=B, H=H, W=W,
+                      mean=(C.c_float * 3)(*mean), std=(C.c_float * 3)(*std), max_pixel=max_pixel_value)
+    _call("maeclip_image_normalize_u8", C.byref(a), _stream())
+    return out
+
+
+def to_device_batch(images_u8, input_ids, attention_mask, device, non_blocking=True):
+    """The dict main.train_epoch feeds the model (main.py:55), built from a
+    host uint8 HWC batch: upload uint8, normalise on the device."""
+    imgs = images_u8.to(device, non_blocking=non_blocking)
+    return {"image": normalize_u8(imgs), "input_ids": input_ids.to(device, non_blocking=non_blocking),
+            "attention_mask": attention_mask.to(device, non_blocking=non_blocking)}

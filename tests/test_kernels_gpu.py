@@ -264,3 +264,44 @@ def test_colsum_two_pass(dev):
     part = _rand((1000, 768), torch.float32, dev, seed=43)
     out = K.colsum_reduce(part)
     assert (out.double() - part.double().sum(0)).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(4, 224, 224), (3, 32, 30), (2, 336, 336), (1, 7, 5)])
+def test_image_normalize_u8_bit_exact(dev, shape):
+    """Device input pipeline (dataset.py:49, 34): uint8 HWC -> normalised fp32
+    NCHW, bit-exact vs the numpy restatement of albumentations' normalize()."""
+    import numpy as np
+    from mae_clip_amd.data import normalize_u8
+    from oracle.input_ref import normalize_u8_ref
+    g = torch.Generator().manual_seed(sum(shape))
+    imgs = torch.randint(0, 256, shape + (3,), generator=g, dtype=torch.uint8)
+    imgs[0, 0, 0] = torch.tensor([0, 255, 128], dtype=torch.uint8)
+    out = normalize_u8(imgs.to(dev)).cpu().numpy()
+    ref = normalize_u8_ref(imgs.numpy())
+    assert out.shape == ref.shape and out.dtype == np.float32
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("QNk", [(1, 6000, 45), (3, 1000, 7), (2, 300, 300)])
+def test_retrieval_normalize_similarity_topk(dev, QNk):
+    """inference.py:40-45 on the device: F.normalize, text_n @ image_n.T, topk
+    (values within fp32 rounding of the fp64 reference; indices equal to the
+    reference order, value descending / index ascending, with planted ties)."""
+    from mae_clip_amd.retrieval import l2_normalize, similarity, topk_rows
+    Q, N, k = QNk
+    t = _rand((Q, 256), torch.float32, dev, seed=91)
+    im = _rand((N, 256), torch.float32, dev, seed=92)
+    im[5] = im[3]          # exact duplicate candidates -> tied scores
+    im[7] = 0.0            # zero row: F.normalize's eps clamp
+    n = l2_normalize(im)
+    ref_n = torch.nn.functional.normalize(im.double(), p=2, dim=-1)
+    assert (n.double() - ref_n).abs().max().item() < 1e-6
+    s = similarity(t, im)
+    ref_s = torch.nn.functional.normalize(t.double(), dim=-1) @ ref_n.T
+    assert (s.double() - ref_s).abs().max().item() < 1e-5
+    vals, idx = topk_rows(s, k)
+    sc = s.double().cpu()
+    for q in range(Q):
+        order = sorted(range(N), key=lambda i: (-sc[q, i].item(), i))[:k]
+        assert idx[q].tolist() == order
+        assert torch.equal(vals[q].cpu(), s[q].cpu()[idx[q].cpu()])

@@ -223,3 +223,67 @@ def test_chunked_stack_matches_whole(dev):
         assert torch.equal(y, outs[0][0]) and torch.equal(gx, outs[0][1])
         for a, b in zip(gp, outs[0][2]):
             assert torch.allclose(a, b, rtol=1e-3, atol=1e-4 * b.abs().max().item())
+
+
+def test_resume_from_checkpoint_is_exact(dev, tmp_path):
+    """Train mode (MAE masks + dropout keyed by the step), HIP AdamW: 4 steps
+    straight == 2 steps, save_checkpoint, fresh model + optimizer,
+    load_checkpoint, 2 steps -- identical losses and final weights."""
+    from tests.helpers import product_config, C0
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.optim import AdamW
+    from mae_clip_amd.checkpoint import save_checkpoint, load_checkpoint
+    kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    batch = {k: v.to(dev) for k, v in make_batch(8, 32).items()}
+
+    def fresh():
+        with product_config(precision="bf16", **kw):
+            torch.manual_seed(0)
+            m = CLIPModel().to(dev).train()
+        return m, AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+
+    def steps(m, opt, n):
+        out = []
+        for _ in range(n):
+            opt.zero_grad(set_to_none=True)
+            loss = m(batch)
+            loss.backward()
+            opt.step()
+            out.append(loss.item())
+        return out
+
+    m, opt = fresh()
+    straight = steps(m, opt, 4)
+    m2, opt2 = fresh()
+    first = steps(m2, opt2, 2)
+    path = tmp_path / "ckpt.pt"
+    save_checkpoint(path, m2, opt2)
+    m3, opt3 = fresh()
+    assert load_checkpoint(path, m3, opt3, map_location=dev) == 2
+    resumed = first + steps(m3, opt3, 2)
+    assert resumed == straight, (resumed, straight)
+    for (k, a), b in zip(m.state_dict().items(), m3.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+def test_inference_find_matches(dev):
+    """inference.py flow on the product model: get_image_embeddings over two
+    batches, then find_matches for one query == torch reference (normalize,
+    matmul, topk(n*5)[::5]) on the same embeddings; image embeddings match the
+    fp64 oracle's image tower + projection."""
+    from mae_clip_amd.retrieval import get_image_embeddings, find_matches
+    prod, ref = build_pair("fp32")
+    b1, b2 = make_batch(8, 32, seed=3), make_batch(8, 32, seed=4)
+    emb = get_image_embeddings(prod, [b1["image"].to(dev), b2["image"].to(dev)])
+    ref.eval()
+    with torch.no_grad():
+        remb = torch.cat([ref.image_projection(ref.image_encoder.model(b["image"].double())) for b in (b1, b2)])
+    assert (emb.double().cpu() - remb).abs().max().item() < 1e-4
+    q = make_batch(1, 32, seed=5)
+    idx = find_matches(prod, emb, q["input_ids"].to(dev), q["attention_mask"].to(dev), n=3)
+    with torch.no_grad():
+        t = prod.text_projection(prod.text_encoder(input_ids=q["input_ids"].to(dev),
+                                                   attention_mask=q["attention_mask"].to(dev)))
+    sim = torch.nn.functional.normalize(t.double(), dim=-1) @ torch.nn.functional.normalize(emb.double(), dim=-1).T
+    order = sorted(range(sim.shape[1]), key=lambda i: (-sim[0, i].item(), i))[:15][::5]
+    assert idx.tolist() == order
