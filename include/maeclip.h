@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 2
+#define MAECLIP_ABI_VERSION 3
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -363,9 +363,15 @@ int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* args, void* stream);
 int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* args, void* stream);
 
 /* ------------------------------------------------------------- CLIP loss
- * CLIPModel.forward loss (CLIP.py:34-43) + cross_entropy (CLIP.py:46-52), fp32.
- * I, T: [N, P] (row strides ld_I/ld_T, 0 = P). loss: device scalar.
- * dI, dT optional (d loss / d I, T; computed in the same call). */
+ * CLIPModel.forward loss (CLIP.py:34-43) + cross_entropy (CLIP.py:46-52), fp32,
+ * fused: no N x N matrix is stored (three all-pairs passes on the exact-f32
+ * MFMA + one reduction launch, deterministic). Any N >= 1; P in {64, 128,
+ * 256, 512}. I, T: [N, P] (row strides ld_I/ld_T, 0 = P, 16-B aligned rows).
+ * loss: device scalar. row_loss_out (optional, [N]): rl_i with loss = sum rl_i.
+ * dI, dT optional: d loss / d I, T for the rows [grad_row0, grad_row0 +
+ * grad_rows) only (grad_rows 0 = to the end), stored from row 0 of dI / dT --
+ * under data parallelism each rank asks for its own slice of the gathered batch.
+ * workspace: >= maeclip_clip_loss_workspace(N, P, number of gradient rows). */
 typedef struct {
   const float* I;
   const float* T;
@@ -377,10 +383,11 @@ typedef struct {
   float* dI;
   float* dT;
   int64_t ld_dI, ld_dT;
+  int64_t grad_row0, grad_rows;
   void* workspace;
   size_t ws_bytes;
 } maeclip_clip_args;
-size_t maeclip_clip_loss_workspace(int64_t N);
+size_t maeclip_clip_loss_workspace(int64_t N, int64_t P, int64_t grad_rows);
 int32_t maeclip_clip_loss(const maeclip_clip_args* args, void* stream);
 
 /* ------------------------------------------------------------ step state

@@ -117,12 +117,12 @@ class CLIPModel(nn.Module):
         mae = self.mae_decoder is not None
         if mae:
             ids_shuffle, ids_restore, mask, keep = self.masking(B, rank * B, img.device)
-            tokens = vit.forward_tokens(img, dtype, cache, ids_shuffle, ids_restore, keep)
+            tokens = vit.forward_tokens(img, dtype, cache, ids_shuffle, ids_restore, keep, world=world)
             dec = self.mae_decoder
             feat, latent = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias,
                                                   dec.mae_norm.weight, dec.mae_norm.bias)
         else:
-            tokens = vit.forward_tokens(img, dtype, cache)
+            tokens = vit.forward_tokens(img, dtype, cache, world=world)
             feat = Fn.EncoderHeadFn.apply(tokens, dtype, vit.fc_norm.weight, vit.fc_norm.bias, None, None)
         if use_side:
             main.wait_stream(side)
@@ -132,11 +132,8 @@ class CLIPModel(nn.Module):
                                               dtype=dtype, step_ptr=sc)
         image_embeddings = self.image_projection(feat, seed=seed + 29, step_ptr=sc)
         text_embeddings = self.text_projection(text_features, seed=seed + 31, step_ptr=sc)
-        if world > 1:
-            from .distributed import gather_rows
-            image_embeddings = gather_rows(image_embeddings, self.process_group)
-            text_embeddings = gather_rows(text_embeddings, self.process_group)
-        clip = clip_loss(image_embeddings, text_embeddings, self.temperature)
+        clip = clip_loss(image_embeddings, text_embeddings, self.temperature,
+                         group=self.process_group if world > 1 else None)
         loss = clip
         self.last_losses = {"clip": clip.detach()}
         if mae:
@@ -144,7 +141,8 @@ class CLIPModel(nn.Module):
             dspec = Fn.DecSpec(B=B, L=L, keep=keep, dtype=dtype, w_T=cache.get(dec.decoder_embed.weight, dtype))
             xd = Fn.DecoderEmbedFn.apply(latent, ids_shuffle, ids_restore, dspec, dec.decoder_embed.weight,
                                          dec.decoder_embed.bias, dec.mask_token, dec.decoder_pos_embed)
-            xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache)
+            xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache,
+                           chunk=(CFG.dp_decoder_chunk or None) if world > 1 else None)
             wp_T, bp_pad = cache.get(dec.decoder_pred.weight, dtype), None
             P = wp_T.shape[0]
             if dtype == torch.bfloat16 and P % 64:
@@ -167,12 +165,15 @@ class CLIPModel(nn.Module):
         return loss
 
 
-def clip_loss(image_embeddings, text_embeddings, temperature=1.0):
-    """CLIP.py:34-43 on the fused fp32 kernel."""
+def clip_loss(image_embeddings, text_embeddings, temperature=1.0, group=None):
+    """CLIP.py:34-43 on the fused fp32 kernel (group: data-parallel gather)."""
     if torch.is_grad_enabled() and (image_embeddings.requires_grad or text_embeddings.requires_grad):
-        return Fn.ClipLossFn.apply(image_embeddings, text_embeddings, temperature)
-    loss, _, _ = K.clip_loss(image_embeddings.contiguous(), text_embeddings.contiguous(), temperature,
-                             want_grad=False)
+        return Fn.ClipLossFn.apply(image_embeddings, text_embeddings, temperature, group)
+    I, T = image_embeddings.contiguous(), text_embeddings.contiguous()
+    if group is not None:
+        from .distributed import all_gather_rows
+        I, T = all_gather_rows(I, group), all_gather_rows(T, group)
+    loss, _, _ = K.clip_loss(I, T, temperature, want_grad=False)
     return loss
 
 

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -104,7 +104,8 @@ class MaeLossArgs(C.Structure):
 class ClipArgs(C.Structure):
     _fields_ = [("I", c_vp), ("T", c_vp), ("ld_I", c_i64), ("ld_T", c_i64), ("N", c_i64), ("P", c_i64),
                 ("temperature", c_f32), ("loss", c_vp), ("row_loss_out", c_vp), ("dI", c_vp), ("dT", c_vp),
-                ("ld_dI", c_i64), ("ld_dT", c_i64), ("workspace", c_vp), ("ws_bytes", c_sz)]
+                ("ld_dI", c_i64), ("ld_dT", c_i64), ("grad_row0", c_i64), ("grad_rows", c_i64),
+                ("workspace", c_vp), ("ws_bytes", c_sz)]
 
 
 class WgradProblem(C.Structure):
@@ -154,7 +155,7 @@ _SIGS = {
     "maeclip_unshuffle_bwd": (c_i32, [C.POINTER(UnshuffleArgs), c_vp]),
     "maeclip_mae_loss_fwd": (c_i32, [C.POINTER(MaeLossArgs), c_vp]),
     "maeclip_mae_loss_bwd": (c_i32, [C.POINTER(MaeLossArgs), c_vp]),
-    "maeclip_clip_loss_workspace": (c_sz, [c_i64]),
+    "maeclip_clip_loss_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "maeclip_clip_loss": (c_i32, [C.POINTER(ClipArgs), c_vp]),
     "maeclip_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
     "maeclip_memcpy_h2d": (c_i32, [c_vp, c_vp, c_sz, c_vp]),

@@ -69,4 +69,5 @@ dropout_seed = 1234
 # ---- scheduling
 side_stream = True         # frozen text tower || image encoder; weight-gradient GEMMs || the dgrad chain
 dp_encoder_chunk = 6       # data parallel: encoder blocks per autograd Function (gradients all-reduced per chunk)
+dp_decoder_chunk = 4       # data parallel: decoder blocks per autograd Function
 wgrad_grouped = True       # all weight gradients of a stack in one grouped GEMM launch (maeclip_wgrad_grouped)

@@ -102,7 +102,7 @@ template <> __device__ __forceinline__ float chunk_dot<float>(v4u a, v4u b) {
 // L2[q] = -lse / c (-1e30 on padding rows), all rows in one pass with every load of an iteration in flight.
 // A row's CPR chunks sit on CPR consecutive lanes of one wave (CPR | 64, NTH a
 // multiple of 64, total a multiple of 64), so the row sum is an xor-shuffle.
-template <typename T, int HD>
+template <typename T, int HD, bool KV>
 __device__ __forceinline__ void bwd_prologue(char* Qi, char* Ki, char* Vi, char* Di, float* L2, float* Dv,
                                              const T* q, const T* k, const T* v, int64_t ld_qkv, const T* O,
                                              const T* dO, int64_t ld_o, const float* lse, float inv_c, int n,
@@ -121,8 +121,10 @@ __device__ __forceinline__ void bwd_prologue(char* Qi, char* Ki, char* Vi, char*
       const int64_t oq = (int64_t)row * ld_qkv + c * EPC, oo = (int64_t)row * ld_o + c * EPC;
       const v4u z = {0, 0, 0, 0};
       vq[u] = ok ? *(const v4u*)(q + oq) : z;
-      vk[u] = ok ? *(const v4u*)(k + oq) : z;
-      vv[u] = ok ? *(const v4u*)(v + oq) : z;
+      if (KV) {
+        vk[u] = ok ? *(const v4u*)(k + oq) : z;
+        vv[u] = ok ? *(const v4u*)(v + oq) : z;
+      }
       vd[u] = ok ? *(const v4u*)(dO + oo) : z;
       vo[u] = ok ? *(const v4u*)(O + oo) : z;
       ls[u] = (ok && c == 0) ? -lse[row] * inv_c : -1.0e30f;
@@ -133,8 +135,10 @@ __device__ __forceinline__ void bwd_prologue(char* Qi, char* Ki, char* Vi, char*
       if (id >= total) break;  // wave-uniform
       const int row = id / CPR, c = id % CPR;
       *(v4u*)(Qi + I::chunk(row, c)) = vq[u];
-      *(v4u*)(Ki + I::chunk(row, c)) = vk[u];
-      *(v4u*)(Vi + I::chunk(row, c)) = vv[u];
+      if (KV) {
+        *(v4u*)(Ki + I::chunk(row, c)) = vk[u];
+        *(v4u*)(Vi + I::chunk(row, c)) = vv[u];
+      }
       *(v4u*)(Di + I::chunk(row, c)) = vd[u];
       float d = chunk_dot<T>(vd[u], vo[u]);
 #pragma unroll
@@ -367,12 +371,17 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int npad = (n + 31) & ~31;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  // bf16: Q, K, V, dO images resident together. fp32 parity mode (rows twice
+  // as wide) holds two at a time so that n = 197 at HD = 64 fits: phase 1
+  // keeps Q, dO in LDS and reads each wave's K/V tile from HBM, phase 2
+  // reloads the two slots with K, V and reads Q/dO tiles from HBM.
+  constexpr bool TWO = !std::is_same<T, bf16_t>::value;
   const int img = npad * I::ROWB;
   char* Qi = smem;
-  char* Ki = smem + img;
-  char* Vi = smem + 2 * img;
-  char* Di = smem + 3 * img;
-  float* L2 = (float*)(smem + 4 * img);
+  char* Di = smem + (TWO ? 1 : 3) * img;
+  char* Ki = TWO ? smem : smem + img;
+  char* Vi = TWO ? smem + img : smem + 2 * img;
+  float* L2 = (float*)(smem + (TWO ? 2 : 4) * img);
   float* Dv = L2 + npad;
   float* cs = Dv + npad;  // [NW][3*HD] bias-grad partials
 
@@ -380,8 +389,8 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
   const T* O = (const T*)a.o + (int64_t)b * n * a.ld_o + h * HD;
   const T* dO = (const T*)a.dout + (int64_t)b * n * a.ld_o + h * HD;
-  bwd_prologue<T, HD>(Qi, Ki, Vi, Di, L2, Dv, qkv + h * HD, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv, O, dO,
-                      a.ld_o, a.lse + ((int64_t)b * H + h) * n, 1.f / (a.scale * LOG2E), n, npad);
+  bwd_prologue<T, HD, !TWO>(Qi, Ki, Vi, Di, L2, Dv, qkv + h * HD, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv,
+                            O, dO, a.ld_o, a.lse + ((int64_t)b * H + h) * n, 1.f / (a.scale * LOG2E), n, npad);
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) cs[i] = 0.f;
   __syncthreads();
 
@@ -397,8 +406,14 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
     RowFrag<T, HD> kf[HD / 32], vf[HD / 32];
 #pragma unroll
     for (int ks = 0; ks < HD / 32; ++ks) {
-      kf[ks].lds(Ki, k0, ks, lane);
-      vf[ks].lds(Vi, k0, ks, lane);
+      if (TWO) {
+        const T* kr = qkv + (int64_t)(kok ? key : 0) * a.ld_qkv + HH + h * HD;
+        kf[ks].glob(kr, ks, lane, kok);
+        vf[ks].glob(kr + HH, ks, lane, kok);
+      } else {
+        kf[ks].lds(Ki, k0, ks, lane);
+        vf[ks].lds(Vi, k0, ks, lane);
+      }
     }
     v4f dv[HD / 16], dk[HD / 16];
 #pragma unroll
@@ -462,6 +477,14 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
     }
   }
 
+  if (TWO) {
+    // phase-1 reads of the Q / dO images are done: K, V take their slots
+    __syncthreads();
+    char* const dst[2] = {Ki, Vi};
+    const T* const src[2] = {qkv + HH + h * HD, qkv + 2 * HH + h * HD};
+    load_imgs<T, HD, 2>(dst, src, a.ld_qkv, n, npad);
+    __syncthreads();
+  }
   // ---------------- phase 2: dQ (wave owns 16-query tiles)
   for (int qt = wave; qt < nkt; qt += NW) {
     const int q0 = qt * 16;
@@ -470,8 +493,13 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
     RowFrag<T, HD> qf[HD / 32], df[HD / 32];
 #pragma unroll
     for (int ks = 0; ks < HD / 32; ++ks) {
-      qf[ks].lds(Qi, q0, ks, lane);
-      df[ks].lds(Di, q0, ks, lane);
+      if (TWO) {
+        qf[ks].glob(qkv + (int64_t)(qok ? q : 0) * a.ld_qkv + h * HD, ks, lane, qok);
+        df[ks].glob(dO + (int64_t)(qok ? q : 0) * a.ld_o, ks, lane, qok);
+      } else {
+        qf[ks].lds(Qi, q0, ks, lane);
+        df[ks].lds(Di, q0, ks, lane);
+      }
     }
     const float lq = L2[q], dq_ = Dv[q];
     v4f dq[HD / 16];
@@ -539,7 +567,8 @@ template <typename T, int HD> size_t fwd_lds(int n) {
 }
 template <typename T, int HD> size_t bwd_lds(int n, int nw) {
   const int npad = (n + 31) & ~31;
-  return (size_t)4 * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
+  const int nimg = std::is_same<T, bf16_t>::value ? 4 : 2;
+  return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
 template <typename T, int HD>

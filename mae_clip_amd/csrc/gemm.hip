@@ -30,7 +30,6 @@
 
 namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
-int gemm_v3(const maeclip_gemm_args& a, hipStream_t s);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
@@ -423,20 +422,17 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
-  // v3/v4/v2 write raw fp32 split-K slabs and leave the reduction to
+  // v4/v2 write raw fp32 split-K slabs and leave the reduction to
   // splitk_reduce (v1's launch() reduces by itself)
   if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small(*a, s);
   int rc = 1;
-  if (a->dtype == MAECLIP_BF16 && forced == 5 && a->epilogue <= EPI_DGELU && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
-      a->M >= 256 && a->N >= 256)
-    rc = maeclip::gemm_v3(*a, s);
   // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
   // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
-  else if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
+  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
     rc = maeclip::gemm_v4(*a, s);
   else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
            (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))
-    rc = maeclip::gemm_v2(*a, s, (forced == 5 || forced == 8) ? 0 : forced);
+    rc = maeclip::gemm_v2(*a, s, forced == 8 ? 0 : forced);
   if (rc != 1) return (rc == 0 && a->splitk > 1) ? splitk_reduce(*a, s) : rc;
   if (a->dtype == MAECLIP_BF16)
     return a->out_dtype == MAECLIP_BF16 ? dispatch_lay<bf16_t, bf16_t>(*a, s) : dispatch_lay<bf16_t, float>(*a, s);

@@ -19,16 +19,33 @@ import torch
 import torch.distributed as dist
 
 
+def world_rank(group=None):
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _staged(group, t):
+    """gloo moves host memory: collectives on device tensors go through a CPU copy."""
+    return dist.get_backend(group) == "gloo" and t.is_cuda
+
+
+def all_gather_rows(x, group=None):
+    """[B, ...] on every rank -> [world*B, ...] in rank order (no autograd)."""
+    world = dist.get_world_size(group)
+    x = x.detach().contiguous()
+    if _staged(group, x):
+        parts = [torch.empty_like(x, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, x.cpu(), group=group)
+        return torch.cat(parts).to(x.device)
+    out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+    dist.all_gather_into_tensor(out, x, group=group)
+    return out
+
+
 class GatherRowsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
-        world = dist.get_world_size(group)
-        rank = dist.get_rank(group)
-        x = x.contiguous()
-        out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
-        dist.all_gather_into_tensor(out, x, group=group)
-        ctx.rank, ctx.n = rank, x.shape[0]
-        return out
+        ctx.rank, ctx.n = dist.get_rank(group), x.shape[0]
+        return all_gather_rows(x, group)
 
     @staticmethod
     def backward(ctx, g):

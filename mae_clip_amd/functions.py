@@ -402,12 +402,29 @@ class ProjectionHeadFn(torch.autograd.Function):
 
 # ------------------------------------------------------------- CLIP loss
 class ClipLossFn(torch.autograd.Function):
+    """CLIP.py:34-43 on the fused fp32 kernel (the gradients come out of the
+    same call; the backward only scales them by grad_output).
+
+    group (data parallel, world > 1): the local [B, P] embeddings of every rank
+    are all-gathered in rank order (the global contrastive denominator, SURVEY
+    §8e), every rank evaluates the loss of the gathered batch and asks the
+    kernel for the gradient of its own B rows only -- so a SUM all-reduce of
+    the parameter gradients is the exact global-batch gradient."""
+
     @staticmethod
-    def forward(ctx, I, T, temperature):
+    def forward(ctx, I, T, temperature, group=None):
         I = I.contiguous()
         T = T.contiguous()
-        need = torch.is_grad_enabled() and (I.requires_grad or T.requires_grad)
-        loss, dI, dT = K.clip_loss(I, T, temperature, want_grad=True)
+        rows = None
+        if group is not None:
+            from .distributed import all_gather_rows, world_rank
+            world, rank = world_rank(group)
+            if world > 1:
+                B = I.shape[0]
+                I = all_gather_rows(I, group)
+                T = all_gather_rows(T, group)
+                rows = (rank * B, B)
+        loss, dI, dT = K.clip_loss(I, T, temperature, want_grad=True, grad_rows=rows)
         ctx.grads = (dI, dT)
         return loss
 
@@ -415,4 +432,4 @@ class ClipLossFn(torch.autograd.Function):
     def backward(ctx, gl):
         dI, dT = ctx.grads
         ctx.grads = None
-        return dI * gl, dT * gl, None
+        return dI * gl, dT * gl, None, None

@@ -35,6 +35,13 @@ class CapturedStep:
         self.static = None
         self.loss = None
         self.calls = 0
+        self.captures = 0
+        self.hp_key = None
+        self.graph_grads = None
+
+    def _hparams(self):
+        """Optimizer hyper-parameters baked into the captured AdamW launch."""
+        return tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in self.opt.param_groups)
 
     def _eager(self, batch):
         self.opt.zero_grad(set_to_none=True)
@@ -47,6 +54,7 @@ class CapturedStep:
         return loss.detach()
 
     def _capture(self, batch):
+        self.graph = None
         self.static = {k: v.clone() for k, v in batch.items()}
         model_step = self.model.step
         # grads are re-created inside the graph's private pool: drop the eager ones
@@ -61,13 +69,32 @@ class CapturedStep:
         self.model.step = model_step
         self.opt._advance_host_steps(-1)
         self.graph, self.loss = g, loss
+        self.hp_key = self._hparams()
+        self.graph_grads = [(p, p.grad) for grp in self.opt.param_groups for p in grp["params"]]
+        self.captures += 1
+
+    def _fits(self, batch):
+        return all(k in self.static and v.shape == self.static[k].shape and v.dtype == self.static[k].dtype
+                   and v.device == self.static[k].device for k, v in batch.items()) and len(batch) == len(self.static)
 
     def step(self, batch):
-        """One training step on `batch` (dict of device tensors); returns the loss tensor."""
+        """One training step on `batch` (dict of device tensors); returns the loss tensor.
+
+        A batch whose shapes differ from the captured ones (e.g. the last,
+        partial batch of an epoch: the reference's DataLoader keeps it,
+        main.py:42-47) runs as an eager step; a change of lr / betas / eps /
+        weight_decay (e.g. by a scheduler, main.py:104) re-captures the graph."""
         self.calls += 1
         if not self.enabled or self.calls <= self.eager_steps:
             return self._eager(batch)
-        if self.graph is None:
+        if self.graph is not None and not self._fits(batch):
+            loss = self._eager(batch)
+            # p.grad of the eager step is not the graph's: point back at the
+            # buffers the next replay fills
+            for p, gr in self.graph_grads:
+                p.grad = gr
+            return loss
+        if self.graph is None or self._hparams() != self.hp_key:
             self._capture(batch)
         else:
             for k, v in batch.items():

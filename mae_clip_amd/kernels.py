@@ -356,18 +356,28 @@ def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=
 
 
 # --------------------------------------------------------------- CLIP loss
-def clip_loss(I, T, temperature, want_grad=True):
+def clip_loss(I, T, temperature, want_grad=True, grad_rows=None, row_loss=False):
+    """Fused soft-target CLIP loss (CLIP.py:34-43). grad_rows = (row0, count):
+    gradients only for that slice of the rows (data parallel: the local rows
+    of the gathered batch); default all rows. Returns (loss, dI, dT[, rl])."""
     _dev(I, T)
     N, P = I.shape
-    ws_bytes = int(L.lib().maeclip_clip_loss_workspace(N))
+    r0, nr = (0, N) if grad_rows is None else grad_rows
+    if not (0 <= r0 and nr >= 1 and r0 + nr <= N):
+        raise ValueError(f"clip_loss: gradient rows {grad_rows} out of range for N={N}")
+    ws_bytes = int(L.lib().maeclip_clip_loss_workspace(N, P, nr if want_grad else 0))
     ws = torch.empty((ws_bytes // 4,), device=I.device, dtype=torch.float32)
     loss = torch.empty((), device=I.device, dtype=torch.float32)
-    dI = torch.empty_like(I) if want_grad else None
-    dT = torch.empty_like(T) if want_grad else None
+    dI = torch.empty((nr, P), device=I.device, dtype=torch.float32) if want_grad else None
+    dT = torch.empty((nr, P), device=I.device, dtype=torch.float32) if want_grad else None
+    rl = torch.empty((N,), device=I.device, dtype=torch.float32) if row_loss else None
     a = L.ClipArgs(I=I.data_ptr(), T=T.data_ptr(), ld_I=I.stride(0), ld_T=T.stride(0), N=N, P=P,
-                   temperature=float(temperature), loss=loss.data_ptr(), row_loss_out=None, dI=_ptr(dI), dT=_ptr(dT),
-                   ld_dI=P, ld_dT=P, workspace=ws.data_ptr(), ws_bytes=ws_bytes)
+                   temperature=float(temperature), loss=loss.data_ptr(), row_loss_out=_ptr(rl), dI=_ptr(dI),
+                   dT=_ptr(dT), ld_dI=P, ld_dT=P, grad_row0=r0, grad_rows=nr, workspace=ws.data_ptr(),
+                   ws_bytes=ws_bytes)
     _call("maeclip_clip_loss", C.byref(a), _stream())
+    if row_loss:
+        return loss, dI, dT, rl
     return loss, dI, dT
 
 

@@ -199,7 +199,7 @@ class VisionTransformer(nn.Module):
             for p in blk.gemm_weights():
                 cache.register(p, p.shape)
 
-    def forward_tokens(self, img, dtype, cache, ids_shuffle=None, ids_restore=None, keep=None):
+    def forward_tokens(self, img, dtype, cache, ids_shuffle=None, ids_restore=None, keep=None, world=1):
         _require_device(img, "image batch")
         B, C, S, S2 = img.shape
         pe = self.patch_embed
@@ -227,10 +227,9 @@ class VisionTransformer(nn.Module):
         spec = Fn.PatchSpec(B=B, L=L, keep=keep, p=pe.patch_size, kpad=kpad, dtype=dtype, w_T=w_T)
         x = Fn.PatchTokensFn.apply(img, ids_shuffle, ids_restore, spec, w, pe.proj.bias, self.cls_token,
                                    self.pos_embed)
-        chunk = None
-        if torch.distributed.is_available() and torch.distributed.is_initialized() and \
-                torch.distributed.get_world_size() > 1:
-            chunk = CFG.dp_encoder_chunk or None
+        # under data parallelism (world = size of the model's process group) the
+        # stack is cut into chunks so upper blocks' gradients reach the all-reduce early
+        chunk = (CFG.dp_encoder_chunk or None) if world > 1 else None
         return run_stack(self.blocks, x, self.num_heads, dtype, cache, chunk=chunk)
 
     def forward(self, img):
@@ -265,10 +264,6 @@ class ImageEncoder(nn.Module):
 
 
 # ------------------------------------------------------------ DistilBERT
-class _Lin(nn.Linear):
-    pass
-
-
 class DistilBertEmbeddings(nn.Module):
     def __init__(self, vocab, dim, max_pos):
         super().__init__()
@@ -472,6 +467,9 @@ class MAEDecoder(nn.Module):
         self.decoder_norm = nn.LayerNorm(dim, eps=1e-6)
         self.decoder_pred = nn.Linear(dim, patch * patch * in_chans)
         nn.init.normal_(self.mask_token, std=0.02)
+        # HF ViTMAEPreTrainedModel._init_weights: every Linear trunc-normal(0.02), zero bias
+        for blk in self.decoder_layers:
+            blk.init_weights()
         _trunc_normal_(self.decoder_embed.weight)
         nn.init.zeros_(self.decoder_embed.bias)
         _trunc_normal_(self.decoder_pred.weight)
@@ -491,8 +489,6 @@ class MAEDecoder(nn.Module):
         pad[0][:P].copy_(w_T)
         pad[1][:P].copy_(self.decoder_pred.bias.detach())
         return pad
-        for blk in self.decoder_layers:
-            blk.init_weights()
 
     def register_weights(self, cache: WeightCache):
         cache.register(self.decoder_embed.weight, self.decoder_embed.weight.shape)

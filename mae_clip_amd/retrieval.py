@@ -47,9 +47,15 @@ def similarity(text_embeddings: torch.Tensor, image_embeddings: torch.Tensor) ->
     im = l2_normalize(image_embeddings.float().contiguous())
     Q, P = tn.shape
     N = im.shape[0]
-    out = torch.empty((Q, N), device=tn.device, dtype=torch.float32)
-    K.gemm(tn, im, out, Q, N, P, tn.stride(0), im.stride(0), N, K.KC, K.KC)
-    return out
+    # the GEMM writes 4-column groups: a gallery of any size is padded with zero
+    # rows to a multiple of 4 and the padded similarity columns are cut off
+    # (a view with row stride Npad: topk_rows honours it)
+    Npad = (N + 3) // 4 * 4
+    if Npad != N:
+        im = torch.cat([im, im.new_zeros((Npad - N, P))])
+    out = torch.empty((Q, Npad), device=tn.device, dtype=torch.float32)
+    K.gemm(tn, im, out, Q, Npad, P, tn.stride(0), im.stride(0), Npad, K.KC, K.KC)
+    return out[:, :N]
 
 
 @torch.no_grad()

@@ -96,11 +96,12 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64)])
+@pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
+                                   (1, 197, 2, 32), (1, 256, 2, 64)])
 def test_attention_fwd_bwd(dev, dtype, shape):
+    """fp32 parity mode holds two [n][hd] f32 images at a time in the
+    backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well."""
     B, n, H, hd = shape
-    if dtype == torch.float32 and n > 100:
-        pytest.skip("fp32 image of this length exceeds LDS (parity runs use short sequences)")
     scale = hd ** -0.5
     qkv = _rand((B * n, 3 * H * hd), dtype, dev, seed=11)
     o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
@@ -159,22 +160,126 @@ def test_layernorm(dev, dtype):
     assert (K.colsum_reduce(pc).double() - dx.double().sum(0)).abs().max().item() < 1e-2
 
 
-def test_clip_loss_kernel_vs_torch(dev):
-    for N in (8, 64, 256):
-        I = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=31), (256,))
-        T = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=32), (256,))
-        loss, dI, dT = K.clip_loss(I, T, 1.0)
-        I64 = I.double().requires_grad_(True)
-        T64 = T.double().requires_grad_(True)
-        logits = T64 @ I64.T
-        tgt = torch.softmax((I64 @ I64.T + T64 @ T64.T) / 2, -1)
-        lt = (-tgt * torch.log_softmax(logits, -1)).sum(1)
-        li = (-tgt.T * torch.log_softmax(logits.T, -1)).sum(1)
-        ref = ((li + lt) / 2).mean()
-        ref.backward()
-        assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
-        assert (dI.double() - I64.grad).abs().max().item() < 1e-5
-        assert (dT.double() - T64.grad).abs().max().item() < 1e-5
+def _clip_ref64(I, T, tau):
+    """CLIP.py:34-43 + cross_entropy (CLIP.py:46-52) in fp64 autograd."""
+    I64 = I.detach().double().cpu().requires_grad_(True)
+    T64 = T.detach().double().cpu().requires_grad_(True)
+    logits = T64 @ I64.T / tau
+    tgt = torch.softmax((I64 @ I64.T + T64 @ T64.T) / 2 * tau, -1)
+    lt = (-tgt * torch.log_softmax(logits, -1)).sum(1)
+    li = (-tgt.T * torch.log_softmax(logits.T, -1)).sum(1)
+    ref = ((li + lt) / 2).mean()
+    ref.backward()
+    return ref.item(), I64.grad, T64.grad
+
+
+@pytest.mark.parametrize("N", [1, 3, 5, 7, 8, 64, 100, 256, 1024, 2048])
+@pytest.mark.parametrize("tau", [1.0, 0.5])
+def test_clip_loss_kernel_vs_torch(dev, N, tau):
+    """Fused CLIP loss (no N x N in HBM) vs fp64 autograd of the reference
+    formula, any N (the reference DataLoader keeps the last partial batch,
+    main.py:42-47), LayerNorm'd 256-d embeddings as the projection heads emit."""
+    I = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=31 + N), (256,))
+    T = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=32 + N), (256,))
+    loss, dI, dT = K.clip_loss(I, T, tau)
+    ref, gI, gT = _clip_ref64(I, T, tau)
+    assert abs(loss.item() - ref) < 1e-5 * max(1.0, abs(ref)), (loss.item(), ref)
+    sc = max(gI.abs().max().item(), gT.abs().max().item())
+    assert (dI.double().cpu() - gI).abs().max().item() < 1e-4 * sc
+    assert (dT.double().cpu() - gT).abs().max().item() < 1e-4 * sc
+    # deterministic: fixed-order partials, bit-identical on a second call
+    loss2, dI2, dT2 = K.clip_loss(I, T, tau)
+    assert torch.equal(loss, loss2) and torch.equal(dI, dI2) and torch.equal(dT, dT2)
+
+
+@pytest.mark.parametrize("N,rows", [(2048, (256, 256)), (1024, (896, 128)), (100, (37, 50)), (256, (0, 256))])
+def test_clip_loss_gradient_rows(dev, N, rows):
+    """Data-parallel form: every rank evaluates the loss of the gathered batch
+    and asks for the gradient of its own row slice only -- equal to that slice
+    of the full gradient, loss identical; no-grad path and per-row losses."""
+    I = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=7), (256,))
+    T = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=8), (256,))
+    lf, dIf, dTf = K.clip_loss(I, T, 1.0)
+    ls, dIs, dTs = K.clip_loss(I, T, 1.0, grad_rows=rows)
+    r0, nr = rows
+    assert torch.equal(lf, ls)
+    assert torch.allclose(dIs, dIf[r0:r0 + nr], rtol=0, atol=1e-6 * dIf.abs().max().item())
+    assert torch.allclose(dTs, dTf[r0:r0 + nr], rtol=0, atol=1e-6 * dTf.abs().max().item())
+    ln, _, _, rl = K.clip_loss(I, T, 1.0, want_grad=False, row_loss=True)
+    assert torch.equal(ln, lf)
+    assert abs(rl.double().sum().item() - lf.item()) < 1e-5 * max(1.0, abs(lf.item()))
+
+
+def test_clip_loss_p128_and_strided(dev):
+    """projection_dim 128 and row-strided inputs (views into a wider buffer)."""
+    N = 40
+    big = torch.nn.functional.layer_norm(_rand((N, 256), torch.float32, dev, seed=9), (256,))
+    I, T = big[:, :128], big[:, 128:]
+    loss, dI, dT = K.clip_loss(I, T, 1.0)
+    ref, gI, gT = _clip_ref64(I, T, 1.0)
+    assert abs(loss.item() - ref) < 1e-5 * max(1.0, abs(ref))
+    sc = max(gI.abs().max().item(), gT.abs().max().item())
+    assert (dI.double().cpu() - gI).abs().max().item() < 1e-4 * sc
+
+
+def test_mask_ids_golden_fixture(dev):
+    """maeclip_mask_ids on the GPU vs tests/golden/masking.npz (HF ViTMAE
+    random_masking on the same counter-based noise, B=32, L=196, keep 49,
+    seed 2, step 3; contains tied keys): noise bits, ids_keep, ids_restore and
+    mask bit-exact."""
+    import numpy as np
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "masking.npz"))
+    B, L_ = z["noise"].shape
+    keep = z["ids_keep"].shape[1]
+    ids_s, ids_r, mask, noise = K.mask_ids(B, L_, keep, seed=2, step=3, sample_offset=0, device=dev, want_noise=True)
+    assert np.array_equal(noise.cpu().numpy().view(np.uint32), z["noise"].view(np.uint32))
+    assert len(np.unique(z["keys24"])) < z["keys24"].size      # the fixture has tied keys
+    assert np.array_equal(ids_s[:, :keep].cpu().long().numpy(), z["ids_keep"])
+    assert np.array_equal(ids_r.cpu().long().numpy(), z["ids_restore"])
+    assert np.array_equal(mask.cpu().numpy(), z["mask"])
+
+
+def test_dropout_statistics(dev):
+    """nn.Dropout semantics of the library's counter-based masks (ProjectionHead
+    p=0.1, modules.py:66,73; DistilBERT hidden/attention dropout p=0.1):
+    drop rate within 5 sigma of p, kept values scaled by 1/(1-p), masks
+    deterministic for a seed and fresh for every device step."""
+    p = 0.1
+    M, D = 4096, 256
+    x = torch.ones((M, D), device=dev)
+    step = torch.zeros(1, dtype=torch.int64, device=dev)
+    y1 = K.dropout(x, p, seed=5, step_ptr=step)
+    y1b = K.dropout(x, p, seed=5, step_ptr=step)
+    K.counter_add(step, 1)
+    y2 = K.dropout(x, p, seed=5, step_ptr=step)
+    n = M * D
+    sig = (p * (1 - p) / n) ** 0.5
+    for y in (y1, y2):
+        frac = (y == 0).float().mean().item()
+        assert abs(frac - p) < 5 * sig, frac
+        kept = y[y != 0]
+        assert torch.allclose(kept, torch.full_like(kept, 1 / (1 - p)))
+    assert torch.equal(y1, y1b)
+    assert not torch.equal(y1, y2)
+    # LayerNorm input dropout (ProjectionHead: dropout(fc(.)) + residual, fused in the LN launch)
+    gamma, beta = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+    _, _, _, _, xs = K.ln_fwd(x, gamma, beta, 1e-5, out_dtype=torch.float32, res=torch.zeros_like(x),
+                              in_dropout=p, seed_in=9, xsum=True, step_ptr=step)
+    frac = (xs == 0).float().mean().item()
+    assert abs(frac - p) < 5 * sig, frac
+    # attention-probability dropout (DistilBERT attention.dropout): q = k = 0 gives
+    # uniform p_k = 1/n, V rows one-hot, so O[q, k] = mask(q, k) / (n (1 - p))
+    B, n, H, hd = 64, 25, 1, 32
+    qkv = torch.zeros((B * n, 3 * H * hd), device=dev)
+    qkv.view(B, n, 3 * hd)[:, :, 2 * hd:2 * hd + n] = torch.eye(n, device=dev)
+    o, _ = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5, dropout_p=p, seed=3, want_lse=False, step_ptr=step)
+    oo = o.view(B, n, hd)[:, :, :n]
+    nz = oo[oo != 0]
+    assert torch.allclose(nz, torch.full_like(nz, 1 / (n * (1 - p))), rtol=1e-5)
+    frac = (oo == 0).float().mean().item()
+    sig2 = (p * (1 - p) / oo.numel()) ** 0.5
+    assert abs(frac - p) < 5 * sig2, frac
 
 
 def test_mask_ids_is_stable_argsort(dev):
@@ -282,7 +387,7 @@ def test_image_normalize_u8_bit_exact(dev, shape):
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("QNk", [(1, 6000, 45), (3, 1000, 7), (2, 300, 300)])
+@pytest.mark.parametrize("QNk", [(1, 6000, 45), (3, 1000, 7), (2, 300, 300), (1, 1001, 45), (2, 9, 9), (1, 7, 3)])
 def test_retrieval_normalize_similarity_topk(dev, QNk):
     """inference.py:40-45 on the device: F.normalize, text_n @ image_n.T, topk
     (values within fp32 rounding of the fp64 reference; indices equal to the
@@ -291,8 +396,8 @@ def test_retrieval_normalize_similarity_topk(dev, QNk):
     Q, N, k = QNk
     t = _rand((Q, 256), torch.float32, dev, seed=91)
     im = _rand((N, 256), torch.float32, dev, seed=92)
-    im[5] = im[3]          # exact duplicate candidates -> tied scores
-    im[7] = 0.0            # zero row: F.normalize's eps clamp
+    im[min(5, N - 1)] = im[3 % N]   # exact duplicate candidates -> tied scores
+    im[N // 2] = 0.0                # zero row: F.normalize's eps clamp
     n = l2_normalize(im)
     ref_n = torch.nn.functional.normalize(im.double(), p=2, dim=-1)
     assert (n.double() - ref_n).abs().max().item() < 1e-6

@@ -51,6 +51,101 @@ def test_c0_parity_fp32(dev, mask_ratio, pad):
     print("worst grad rel err:", worst[:3])
 
 
+def _grad_errs(prod, ref):
+    """max-abs relative error of every trainable gradient (vs the oracle's)."""
+    rp = dict(ref.named_parameters())
+    out = []
+    for name, p in prod.named_parameters():
+        if not p.requires_grad:
+            continue
+        assert p.grad is not None and rp[name].grad is not None, name
+        rg = rp[name].grad
+        out.append(((p.grad.double().cpu() - rg).abs().max().item() / (rg.abs().max().item() + 1e-30), name))
+    return sorted(out, reverse=True)
+
+
+def test_c0_parity_norm_pix_fp32(dev):
+    """HF ViTMAE loss with norm_pix_loss=True (modeling_vit_mae.py:852-859:
+    per-patch mean / unbiased var, eps 1e-6) through the product at C0."""
+    prod, ref = build_pair("fp32", norm_pix_loss=True)
+    prod.eval()
+    ref.eval()
+    loss, rloss = _run(prod, ref, make_batch(8, 32), dev)
+    assert abs(loss.item() - rloss.item()) < 1e-5 * max(1.0, abs(rloss.item())), (loss.item(), rloss.item())
+    assert abs(prod.last_losses["mae"].item() - ref.last_losses["mae"].item()) < 1e-5
+    worst = _grad_errs(prod, ref)
+    assert worst[0][0] < 1e-3, worst[:3]
+
+
+@pytest.mark.parametrize("B", [1, 5, 7])
+def test_c0_parity_odd_batch(dev, B):
+    """Batch sizes the reference's DataLoader produces at the end of an epoch
+    (drop_last=False, main.py:42-47): any B reaches the fused CLIP loss."""
+    prod, ref = build_pair("fp32")
+    prod.eval()
+    ref.eval()
+    loss, rloss = _run(prod, ref, make_batch(B, 32, seed=B), dev)
+    assert abs(loss.item() - rloss.item()) < 1e-5 * max(1.0, abs(rloss.item())), (loss.item(), rloss.item())
+    worst = _grad_errs(prod, ref)
+    assert worst[0][0] < 1e-3, worst[:3]
+
+
+VITB_C1 = dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6, mask_ratio=0.0)
+VITB_C2 = dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6, mask_ratio=0.75,
+               decoder_embed_dim=512, decoder_depth=8, decoder_num_heads=16)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_vitb_parity_fp32_vs_oracle(dev, cfg):
+    """BASELINE configs[1]/[2] model shapes (ViT-B/16 @224: n = 197 / 50 encoder
+    tokens, 8x512-d decoder at n = 197 with hd 32, 6-layer text) in fp32 parity
+    mode vs the fp64 CPU oracle on identical weights, B = 2: C1 is the
+    reference's own CLIP path (CLIP.py:23-43 with modules.py:17-19, mask 0).
+    |dloss| <= 1e-3 (north_star) and every trainable gradient <= 1e-3 max-rel."""
+    kw = VITB_C1 if cfg == "C1" else VITB_C2
+    prod, ref = build_pair("fp32", **kw)
+    prod.eval()
+    ref.eval()
+    loss, rloss = _run(prod, ref, make_batch(2, 224, seed=11), dev)
+    d = abs(loss.item() - rloss.item())
+    assert d < 1e-3 and d < 1e-5 * max(1.0, abs(rloss.item())), (loss.item(), rloss.item())
+    if cfg == "C2":
+        ids_s, ids_r, mask = prod.last_mask
+        r_s, r_r, r_m, _ = ref.mask_for_batch(2, 0)
+        assert torch.equal(ids_s.cpu().long(), r_s) and torch.equal(mask.cpu(), r_m)
+    worst = _grad_errs(prod, ref)
+    print(cfg, "fp32 |dloss|", d, "worst grads", worst[:3])
+    assert worst[0][0] < 1e-3, worst[:5]
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_vitb_bf16_vs_oracle(dev, cfg):
+    """The bench's bf16 production path at ViT-B shapes vs the fp64 oracle on
+    identical weights (B = 4). Tolerances (bf16 GEMM operands, fp32
+    accumulation and statistics; SURVEY.md §7 'Parity vs bf16'): loss within
+    2e-2 relative; every gradient within 1e-1 relative L2 of the oracle's."""
+    kw = VITB_C1 if cfg == "C1" else VITB_C2
+    prod, ref = build_pair("bf16", **kw)
+    prod.eval()
+    ref.eval()
+    loss, rloss = _run(prod, ref, make_batch(4, 224, seed=12), dev)
+    rel = abs(loss.item() - rloss.item()) / max(1.0, abs(rloss.item()))
+    rp = dict(ref.named_parameters())
+    bad = []
+    worst = 0.0
+    for name, p in prod.named_parameters():
+        if not p.requires_grad:
+            continue
+        rg = rp[name].grad
+        e = ((p.grad.double().cpu() - rg).norm() / (rg.norm() + 1e-30)).item()
+        worst = max(worst, e)
+        if not e < 1e-1:
+            bad.append((e, name))
+    print(cfg, "bf16 loss rel", rel, "worst grad rel-L2", worst)
+    assert rel < 2e-2, (loss.item(), rloss.item())
+    assert not bad, sorted(bad, reverse=True)[:5]
+
+
 def test_c0_bf16_close(dev):
     prod, ref = build_pair("bf16")
     prod.eval()
@@ -155,6 +250,39 @@ def test_training_curve_fp32(dev):
         rl.backward()
         ropt.step()
         assert abs(l.item() - rl.item()) < 1e-3, (it, l.item(), rl.item())
+
+
+def test_captured_step_partial_batch_and_lr_change(dev):
+    """CapturedStep: a batch of another size runs eagerly instead
+    of being broadcast into the static buffers, and an lr change after capture
+    (a scheduler, main.py:104) takes effect -- same losses and weights as an
+    all-eager run of the same sequence."""
+    from tests.helpers import product_config, C0
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.optim import AdamW
+    from mae_clip_amd.graph import CapturedStep
+    kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    sizes = [8, 8, 8, 5, 8, 8, 1, 8]
+    runs = []
+    for captured in (False, True):
+        with product_config(precision="fp32", **kw):
+            torch.manual_seed(0)
+            m = CLIPModel().to(dev).train()
+        opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+        runner = CapturedStep(m, opt, enabled=captured)
+        losses = []
+        for it, B in enumerate(sizes):
+            if it == 5:
+                for g in opt.param_groups:
+                    g["lr"] = 5e-4
+            batch = {k: v.to(dev) for k, v in make_batch(B, 32, seed=it).items()}
+            losses.append(runner.step(batch).item())
+        runs.append((losses, m, runner))
+    (le, me, _), (lg, mg, rg) = runs
+    assert le == lg, (le, lg)
+    assert rg.captures == 2          # initial capture + the re-capture after the lr change
+    for (n1, p1), (n2, p2) in zip(me.named_parameters(), mg.named_parameters()):
+        assert torch.equal(p1, p2), n1
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
