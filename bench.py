@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md; 6.3 TB/s measured copy)
 PEAK_F32_TFLOPS = 157.3
 IMG_FLOPS_C2 = 60.2e9       # algorithmic FLOP / image, SURVEY.md §8d / Appendix C
 
@@ -69,11 +70,23 @@ def parity_c0(device):
     return abs(lp - lr), lp, lr
 
 
+def cpu_model_name():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(seconds_budget=20.0):
     """The CPU oracle (pure torch fp32, same ops as the reference) on a bounded
-    sample of the same workload: ViT-B/16 MAE+CLIP, 6-layer text, B=16."""
+    sample of the same workload: ViT-B/16 MAE+CLIP, 6-layer text, B=16.
+    Threads = the job's CPU share (OMP_NUM_THREADS, 16 on the GPU box; the
+    box's os.cpu_count() is the whole host's, several jobs share it)."""
     from oracle.ref_model import CLIPModel as RefCLIP, OracleConfig
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     cfg = OracleConfig(model_name="vit_base_patch16_224", img_size=224, text_layers=6, mask_ratio=0.75,
                        decoder_dim=512, decoder_depth=8, decoder_heads=16)
@@ -96,7 +109,9 @@ def cpu_baseline(seconds_budget=20.0):
             break
     timed = times[1:] if len(times) > 1 else times
     per_step = sorted(timed)[len(timed) // 2]
-    return {"value": B / per_step, "unit": "images/s", "cores": threads, "kind": "port",
+    return {"value": B / per_step, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model_name(),
+            "calibration": "profiles/r02/cpu_calibration.json",
             "sample": f"oracle ViT-B/16 MAE+CLIP + 6-layer text, fp32 CPU, B={B}, median of {len(timed)} "
                       f"step(s) after 1 warm-up (fwd+bwd+AdamW)"}
 
@@ -114,7 +129,7 @@ def pmc_traffic(key):
             r = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if r.get("shape") == key and (best is None or os.path.getmtime(f) >= os.path.getmtime(best[0])):
+        if r.get("shape", "").split(">")[0] == key.split(">")[0] and (best is None or os.path.getmtime(f) >= os.path.getmtime(best[0])):
             best = (f, r)
     if best is None:
         return None, None
@@ -139,7 +154,7 @@ class KernelTimer:
         self.captured = []   # (key, flops, slot) bracketed inside the graph
         self.ts = None       # device int64 [2 * slots] timestamps
 
-    def hook(self, key, flops, launch):
+    def hook(self, key, flops, nbytes, launch):
         if not self.active or (self.only is not None and key != self.only):
             return launch()
         from mae_clip_amd.functions import side_stream
@@ -158,13 +173,13 @@ class KernelTimer:
             _lib.check(lib.maeclip_timestamp(self.ts.data_ptr() + 16 * i, st), "maeclip_timestamp")
             launch()
             _lib.check(lib.maeclip_timestamp(self.ts.data_ptr() + 16 * i + 8, st), "maeclip_timestamp")
-            self.captured.append((key, flops, i))
+            self.captured.append((key, flops, nbytes, i))
             return
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.records.setdefault(key, [flops, []])[1].append((s, e))
+        self.records.setdefault(key, [flops, nbytes, []])[2].append((s, e))
 
     def harvest(self):
         """After a synchronised replay: add the captured launches' durations (ms)."""
@@ -173,27 +188,44 @@ class KernelTimer:
         from mae_clip_amd import _lib
         khz = float(_lib.lib().maeclip_wallclock_khz()) or 100000.0
         t = self.ts.view(-1, 2).cpu()
-        for key, flops, i in self.captured:
-            self.records.setdefault(key, [flops, []])[1].append(float(t[i, 1] - t[i, 0]) / khz)
+        for key, flops, nbytes, i in self.captured:
+            self.records.setdefault(key, [flops, nbytes, []])[2].append(float(t[i, 1] - t[i, 0]) / khz)
 
     def table(self, steps, file):
         rows = []
-        for key, (flops, evs) in self.records.items():
+        for key, (flops, nbytes, evs) in self.records.items():
             ms = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in evs]
-            rows.append((sum(ms) / steps, len(ms) / steps, flops / (sum(ms) / len(ms)) / 1e9, key))
+            avg = sum(ms) / len(ms)
+            rows.append((sum(ms) / steps, len(ms) / steps, flops / avg / 1e9, nbytes / avg / 1e6, key))
         rows.sort(reverse=True)
         print(f"GEMM total {sum(r[0] for r in rows):.3f} ms/step", file=file)
-        for t, n, tf, key in rows:
-            print(f"{t:8.3f} ms/step {n:5.1f} launches/step {tf:7.1f} TF/s  {key}", file=file)
+        for t, n, tf, gbs, key in rows:
+            print(f"{t:8.3f} ms/step {n:5.1f} launches/step {tf:7.1f} TF/s {gbs:7.1f} GB/s  {key}", file=file)
 
     def summary(self):
         best = None
-        for key, (flops, evs) in self.records.items():
+        for key, (flops, nbytes, evs) in self.records.items():
             ms = [x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in evs]
             tot = sum(ms)
             if best is None or tot > best[2]:
-                best = (key, flops, tot, len(ms))
+                best = (key, flops, tot, len(ms), nbytes)
         return best
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks through
+    torch.distributed.run (one process per GPU) and relay rank 0's JSON line.
+    The parent never touches the GPU (no HIP context before the children)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -213,6 +245,11 @@ def main():
     ap.add_argument("--no-side-stream", action="store_true",
                     help="text tower and weight gradients on the main stream (config.side_stream = False)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started WORLD_SIZE="
+                         f"{os.environ.get('WORLD_SIZE')} ranks")
     # the driver reads ONE JSON line from stdout: route everything else written
     # to fd 1 (RCCL's version banner, library chatter) to stderr
     sys.stdout.flush()
@@ -306,13 +343,24 @@ def main():
         roof = None
         best = timer.summary() if not args.no_kernel_timer else None
         if best is not None:
-            key, flops, tot_ms, nl = best
+            key, flops, tot_ms, nl, nbytes = best
             avg_s = tot_ms / nl / 1000.0
-            ach = flops / avg_s / 1e12
+            tf = flops / avg_s / 1e12
+            gbs = nbytes / avg_s / 1e9
+            # which roof bounds it: arithmetic intensity vs the ridge point
+            ai = flops / nbytes
+            ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
             traffic, tsrc = pmc_traffic(key)
-            roof = {"bound": "mfma", "kernel": "gemm " + key, "achieved": round(ach, 1),
-                    "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                    "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+            if ai >= ridge:
+                bound, ach, peak, unit = "mfma", tf, PEAK_BF16_TFLOPS, "TFLOP/s"
+            else:
+                bound, ach, peak, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
+            roof = {"bound": bound, "kernel": "gemm " + key, "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                    "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                    "traffic_source": tsrc, "algorithmic_bytes": nbytes, "flops": flops,
+                    "arith_intensity": round(ai, 1), "ridge": round(ridge, 1),
+                    "tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4), "gbs": round(gbs, 1),
+                    "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
                     "avg_launch_us": round(avg_s * 1e6, 1), "launches": nl,
                     "step_tflops": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12, 1),
                     "step_frac": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12 / PEAK_BF16_TFLOPS, 4)}
@@ -324,7 +372,9 @@ def main():
                                       "T=25, AdamW, bf16 MFMA / fp32 master",
                           "global_batch": global_batch, "per_gpu_batch": args.batch, "image_size": 224,
                           "mask_ratio": args.mask_ratio, "parallelism": f"dp{world}"},
-               "loss": round(loss.item(), 4), "roofline": roof}
+               "loss": round(loss.item(), 4), "roofline": roof,
+               "step_mode": "hip-graph" if use_graph else "eager",
+               "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size()} if use_dp else None}
         if world == 1 and not args.no_parity:
             try:
                 dl, lp, lr = parity_c0(device)

@@ -61,6 +61,7 @@ class CLIPModel(nn.Module):
         self.register_buffer("step_counter", torch.zeros(1, dtype=torch.int64), persistent=False)
         self.last_losses = {}
         self.process_group = None
+        self.grad_arena = None     # set by distributed.DataParallel (flat all-reduce buffer)
         self._cache = None
 
     # ------------------------------------------------------------------
@@ -96,6 +97,7 @@ class CLIPModel(nn.Module):
         vit = self.image_encoder.model
         B = img.shape[0]
         world, rank = self._world()
+        Fn.set_grad_arena(self.grad_arena if torch.is_grad_enabled() else None)
         sc = self.step_counter
         if not sc.is_cuda:
             raise RuntimeError("CLIPModel.step_counter must live on the GPU (call .to(device))")

@@ -57,8 +57,45 @@ def gather_rows(x, group=None):
     return GatherRowsFn.apply(x, group)
 
 
+class GradArena:
+    """All trainable gradients in one flat fp32 buffer, laid out in reverse
+    registration order (~ the order the backward produces them), so that every
+    all-reduce bucket is one contiguous slice. slot(p) hands a Function's
+    backward a fresh view of p's range to write the gradient into."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        self.offsets = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = (off, p.numel(), tuple(p.shape))
+            off += p.numel()
+        self.flat = torch.zeros(off, device=device, dtype=torch.float32)
+
+    def view(self, p):
+        off, n, shape = self.offsets[id(p)]
+        return self.flat[off:off + n].view(shape)
+
+    def slot(self, p):
+        e = self.offsets.get(id(p))
+        if e is None or p.grad is not None or p.dtype != torch.float32:
+            return None
+        return self.view(p)
+
+    def owns(self, p):
+        g = p.grad
+        return g is not None and g.data_ptr() == self.flat.data_ptr() + 4 * self.offsets[id(p)][0]
+
+
 class DataParallel:
     """Gradient synchroniser for a model replicated on every rank.
+
+    The gradients live in a GradArena: the product's autograd Functions write
+    each parameter's gradient directly into its slot (autograd adopts the slot
+    as p.grad), so a bucket is all-reduced in place on a slice of the flat
+    buffer -- no flatten / unflatten copies. Gradients produced elsewhere (the
+    CPU oracle modules of the gloo tests, gradient accumulation) are copied
+    into their slots first and back afterwards.
 
     bucket_mb: gradient bytes per all-reduce. xGMI is point-to-point (7 links x
     ~153 GB/s per MI355X), so a ring all-reduce is per-link bound; 64 MB buckets
@@ -75,12 +112,21 @@ class DataParallel:
         if broadcast:
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
-                    dist.broadcast(t, src=0, group=group)
-        # buckets in reverse registration order (~ the order grads become ready)
+                    if _staged(group, t):
+                        h = t.detach().cpu()
+                        dist.broadcast(h, src=0, group=group)
+                        t.copy_(h)
+                    else:
+                        dist.broadcast(t, src=0, group=group)
+        order = list(reversed(self.params))
+        self.arena = GradArena(order, self.params[0].device)
+        if hasattr(model, "grad_arena"):
+            model.grad_arena = self.arena
+        # buckets = contiguous arena ranges in reverse registration order
         cap = int(bucket_mb * 2 ** 20)
         self.buckets, cur, size = [], [], 0
-        for p in reversed(self.params):
-            nb = p.numel() * p.element_size()
+        for p in order:
+            nb = p.numel() * 4
             if cur and size + nb > cap:
                 self.buckets.append(cur)
                 cur, size = [], 0
@@ -88,11 +134,17 @@ class DataParallel:
             size += nb
         if cur:
             self.buckets.append(cur)
+        self.ranges = []
+        for b in self.buckets:
+            o0 = self.arena.offsets[id(b[0])][0]
+            o1 = self.arena.offsets[id(b[-1])][0] + b[-1].numel()
+            self.ranges.append((o0, o1))
         self._bucket_of = {id(p): i for i, b in enumerate(self.buckets) for p in b}
         self._pending = [0] * len(self.buckets)
         self._works = []
-        self._flats = [None] * len(self.buckets)
+        self._copied = [[] for _ in self.buckets]
         self.overlap = True
+        self.adopted = 0      # gradients that arrived already in their arena slot (last step)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def _on_grad(self, p):
@@ -104,26 +156,43 @@ class DataParallel:
             self._launch(i)
 
     def _launch(self, i):
-        grads = [p.grad for p in self.buckets[i]]
-        flat = torch._utils._flatten_dense_tensors(grads)
-        self._flats[i] = flat
-        self._works.append((i, dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)))
+        copied = []
+        for p in self.buckets[i]:
+            if p.grad is None:
+                self.arena.view(p).zero_()
+                p.grad = self.arena.view(p)
+            elif self.arena.owns(p):
+                self.adopted += 1
+            else:
+                self.arena.view(p).copy_(p.grad)
+                copied.append(p)
+        self._copied[i] = copied
+        o0, o1 = self.ranges[i]
+        buf = self.arena.flat[o0:o1]
+        if _staged(self.group, buf):
+            host = buf.cpu()
+            w = dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._works.append((i, w, host))
+        else:
+            w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._works.append((i, w, None))
 
     def sync_gradients(self):
         """Finish (or, with overlap off, perform) the SUM all-reduce of all grads."""
-        launched = {i for i, _ in self._works}
+        launched = {i for i, _, _ in self._works}
         for i in range(len(self.buckets)):
             if i not in launched:
-                if any(p.grad is None for p in self.buckets[i]):
-                    for p in self.buckets[i]:
-                        if p.grad is None:
-                            p.grad = torch.zeros_like(p)
                 self._launch(i)
-        for i, w in self._works:
+        for i, w, host in self._works:
             w.wait()
-            grads = [p.grad for p in self.buckets[i]]
-            # one multi-tensor copy per bucket (not one launch per parameter)
-            torch._foreach_copy_(grads, torch._utils._unflatten_dense_tensors(self._flats[i], grads))
+            if host is not None:
+                o0, o1 = self.ranges[i]
+                self.arena.flat[o0:o1].copy_(host)
+            for p in self._copied[i]:
+                p.grad.copy_(self.arena.view(p))
         self._works = []
-        self._flats = [None] * len(self.buckets)
+        self._copied = [[] for _ in self.buckets]
         self._pending = [0] * len(self.buckets)
+
+    def reset_stats(self):
+        self.adopted = 0

@@ -25,8 +25,37 @@ import torch
 from . import kernels as K
 
 
-def _reduce(part):
-    return K.colsum_reduce(part)
+def _reduce(part, out=None):
+    return K.colsum_reduce(part, out=out)
+
+
+# --------------------------------------------------------- gradient arena
+# Data parallel (mae_clip_amd.distributed.DataParallel) keeps every trainable
+# gradient in ONE flat fp32 buffer; the backward of each Function below writes
+# a parameter's gradient straight into that parameter's slot, autograd adopts
+# the slot as p.grad, and the bucketed all-reduce runs on slices of the flat
+# buffer -- no flatten / unflatten copies. Without an arena (single GPU) every
+# gradient is a fresh tensor as before.
+_ARENA = [None]
+
+
+def set_grad_arena(arena):
+    _ARENA[0] = arena
+
+
+def _arena():
+    return _ARENA[0]
+
+
+def gout(arena, p, shape=None):
+    """Output buffer for p's gradient: its arena slot (a fresh view object, so
+    autograd's AccumulateGrad adopts it without a copy) when p.grad is None,
+    else a new tensor (gradient accumulation adds it to the existing p.grad)."""
+    if arena is not None:
+        v = arena.slot(p)
+        if v is not None:
+            return v if shape is None else v.view(shape)
+    return torch.empty(shape if shape is not None else p.shape, device=p.device, dtype=torch.float32)
 
 
 # ------------------------------------------------------------ side stream
@@ -64,17 +93,19 @@ class WgradQueue:
         self.grouped = grouped
         self.items = []
 
-    def wgrad(self, dy, x):
+    def wgrad(self, dy, x, out=None):
         if self.grouped:
-            out = torch.empty((dy.shape[1], x.shape[1]), device=dy.device, dtype=torch.float32)
+            if out is None:
+                out = torch.empty((dy.shape[1], x.shape[1]), device=dy.device, dtype=torch.float32)
             if self.items and self.items[0][0].shape[0] != dy.shape[0]:
                 self.flush()
             self.items.append((dy, x, out))
             return out
         if self.side is None:
-            return K.linear_wgrad(dy, x)
+            return K.linear_wgrad(dy, x, out=out)
         M, N = dy.shape
-        out = torch.empty((N, x.shape[1]), device=dy.device, dtype=torch.float32)
+        if out is None:
+            out = torch.empty((N, x.shape[1]), device=dy.device, dtype=torch.float32)
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             K.linear_wgrad(dy, x, out=out)
@@ -138,6 +169,7 @@ class TransformerStackFn(torch.autograd.Function):
         ctx.saved = saved
         ctx.spec = spec
         ctx.params = params
+        ctx.arena = _arena()
         return xi.view(B, n, D)
 
     @staticmethod
@@ -166,40 +198,42 @@ class TransformerStackFn(torch.autograd.Function):
             n1w, n2w = p[0], p[6]
             xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
             gi = [None] * PER_BLOCK
+            ar = ctx.arena
             # mlp.fc2 (+ GELU backward fused into the dgrad epilogue: dA = (dy W2) * gelu'(h))
-            gi[11] = rb.add(cpart)
+            gi[11] = rb.add(cpart, out=gout(ar, p[11]))
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
             dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
-            gi[10] = wq.wgrad(gT, a)
+            gi[10] = wq.wgrad(gT, a, out=gout(ar, p[10]))
             del a, dgelu
             # mlp.fc1
-            gi[9] = rb.add(dA_part)
+            gi[9] = rb.add(dA_part, out=gout(ar, p[9]))
             dh2 = K.linear_dgrad(dA, w1)
-            gi[8] = wq.wgrad(dA, h2)
+            gi[8] = wq.wgrad(dA, h2, out=gout(ar, p[8]))
             del dA
             # norm2 (+ residual gradient)
             dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True)
-            gi[6], gi[7] = rb.add(pg), rb.add(pb)
+            gi[6], gi[7] = rb.add(pg, out=gout(ar, p[6])), rb.add(pb, out=gout(ar, p[7]))
             if not bf:
                 dx1T = dx1
             # attn.proj
-            gi[5] = rb.add(pc)
+            gi[5] = rb.add(pc, out=gout(ar, p[5]))
             dO = K.linear_dgrad(dx1T, wproj)
-            gi[4] = wq.wgrad(dx1T, o)
+            gi[4] = wq.wgrad(dx1T, o, out=gout(ar, p[4]))
             # attention
             dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
             del dO
-            gi[3] = rb.add(qpart)
+            gi[3] = rb.add(qpart, out=gout(ar, p[3]))
             dh1 = K.linear_dgrad(dqkv, wqkv)
-            gi[2] = wq.wgrad(dqkv, h1)
+            gi[2] = wq.wgrad(dqkv, h1, out=gout(ar, p[2]))
             del dqkv
             # norm1 (+ residual gradient)
             dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True)
-            gi[0], gi[1] = rb.add(pg), rb.add(pb)
+            gi[0], gi[1] = rb.add(pg, out=gout(ar, p[0])), rb.add(pb, out=gout(ar, p[1]))
             ctx.saved[i] = None
             g, gT, cpart = dx, (dxT if bf else dx), pc
             for j in range(PER_BLOCK):
                 grads[i * PER_BLOCK + j] = gi[j].view(p[j].shape)
+            del gi
         rb.flush()
         wq.join()
         ctx.saved = None
@@ -227,6 +261,8 @@ class PatchTokensFn(torch.autograd.Function):
         ctx.save = (Xp, ids_restore)
         ctx.spec = spec
         ctx.wshape = w.shape
+        ctx.params = (w, b, cls, pos)
+        ctx.arena = _arena()
         return x
 
     @staticmethod
@@ -234,14 +270,19 @@ class PatchTokensFn(torch.autograd.Function):
         spec = ctx.spec
         Xp, ids_restore = ctx.save
         gx = gx.contiguous()
-        dY, dpos, dcls = K.tokens_bwd(gx, ids_restore, spec.B, spec.L, spec.keep, spec.dtype)
-        dW = K.linear_wgrad(dY, Xp)
+        w, b, cls, pos = ctx.params
+        ar = ctx.arena
+        D = pos.shape[-1]
+        dY, dpos, dcls = K.tokens_bwd(gx, ids_restore, spec.B, spec.L, spec.keep, spec.dtype,
+                                      dpos=gout(ar, pos, (spec.L + 1, D)), dcls=gout(ar, cls, (D,)))
         Kreal = ctx.wshape[1] * ctx.wshape[2] * ctx.wshape[3]
+        dWo = gout(ar, w, (ctx.wshape[0], Kreal))
         if Kreal != spec.kpad:
-            dW = dW[:, :Kreal].contiguous()
-        db = _reduce(K.rows_colsum(dY))
-        D = dpos.shape[-1]
-        return None, None, None, None, dW.view(ctx.wshape), db, dcls.view(1, 1, D), dpos.view(1, -1, D)
+            dWo.copy_(K.linear_wgrad(dY, Xp)[:, :Kreal])
+        else:
+            K.linear_wgrad(dY, Xp, out=dWo)
+        db = _reduce(K.rows_colsum(dY), out=gout(ar, b))
+        return None, None, None, None, dWo.view(ctx.wshape), db, dcls.view(1, 1, D), dpos.view(1, -1, D)
 
 
 # ------------------------------------------------------- encoder outputs
@@ -260,6 +301,8 @@ class EncoderHeadFn(torch.autograd.Function):
             ctx.lstats = (lm, lr)
         ctx.save = (x, pooled, fm, fr)
         ctx.w = (fcn_w, mn_w)
+        ctx.b = (fcn_b, mn_b)
+        ctx.arena = _arena()
         if latent is None:
             return feat
         return feat, latent
@@ -271,14 +314,16 @@ class EncoderHeadFn(torch.autograd.Function):
         B, n, D = x.shape
         dpooled, _, pg, pb, _ = K.ln_bwd(gfeat.contiguous(), pooled, fm, fr, fcn_w)
         dx = K.pool_bwd(dpooled, n)
-        g_fw, g_fb = _reduce(pg), _reduce(pb)
+        fcn_b, mn_b = ctx.b
+        ar = ctx.arena
+        g_fw, g_fb = _reduce(pg, out=gout(ar, fcn_w)), _reduce(pb, out=gout(ar, fcn_b))
         g_mw = g_mb = None
         if ctx.mae and glatent is not None:
             lm, lr = ctx.lstats
             dx2, _, pg2, pb2, _ = K.ln_bwd(glatent.contiguous(), x.view(B * n, D), lm, lr, mn_w,
                                            dres=dx.view(B * n, D))
             dx = dx2.view(B, n, D)
-            g_mw, g_mb = _reduce(pg2), _reduce(pb2)
+            g_mw, g_mb = _reduce(pg2, out=gout(ar, mn_w)), _reduce(pb2, out=gout(ar, mn_b))
         return dx, None, g_fw, g_fb, g_mw, g_mb
 
 
@@ -300,6 +345,8 @@ class DecoderEmbedFn(torch.autograd.Function):
                              spec.keep)
         ctx.save = (latent, ids_shuffle)
         ctx.spec = spec
+        ctx.params = (w, b, mask_token)
+        ctx.arena = _arena()
         return xd
 
     @staticmethod
@@ -307,10 +354,12 @@ class DecoderEmbedFn(torch.autograd.Function):
         spec = ctx.spec
         latent, ids_shuffle = ctx.save
         dy, dmask_part, cs = K.unshuffle_bwd(gxd.contiguous(), ids_shuffle, spec.B, spec.L, spec.keep, spec.dtype)
+        w, b, mask_token = ctx.params
+        ar = ctx.arena
         dlatent = K.linear_dgrad(dy, spec.w_T)
-        dW = K.linear_wgrad(dy, latent)
-        db = _reduce(cs)
-        dmask = _reduce(dmask_part)
+        dW = K.linear_wgrad(dy, latent, out=gout(ar, w))
+        db = _reduce(cs, out=gout(ar, b))
+        dmask = _reduce(dmask_part, out=gout(ar, mask_token, (mask_token.shape[-1],)))
         return dlatent, None, None, None, dW, db, dmask.view(1, 1, -1), None
 
 
@@ -339,6 +388,8 @@ class MaeHeadLossFn(torch.autograd.Function):
         ctx.dn_w = dn_w
         ctx.shape = xd.shape
         ctx.P = wp.shape[0]
+        ctx.params = (dn_w, dn_b, wp, bp)
+        ctx.arena = _arena()
         return loss
 
     @staticmethod
@@ -347,13 +398,19 @@ class MaeHeadLossFn(torch.autograd.Function):
         x2, h, m, r, pred, img, mask = ctx.save
         dpred, cs = K.mae_loss_bwd(pred, img, mask, spec.p, spec.norm_pix, gl.contiguous(), spec.mask_count,
                                    spec.loss_scale)
+        dn_w, dn_b, wp, bp = ctx.params
+        ar = ctx.arena
         dh = K.linear_dgrad(dpred, spec.w_T)
-        dWp = K.linear_wgrad(dpred, h)
-        if dWp.shape[0] != ctx.P:
-            dWp = dWp[:ctx.P].contiguous()
-        dbp = _reduce(cs)
+        dWp = gout(ar, wp)
+        if dpred.shape[1] != ctx.P:      # padded pred rows (patch 14): slice back
+            dWp.copy_(K.linear_wgrad(dpred, h)[:ctx.P])
+            dbp = _reduce(cs[:, :ctx.P].contiguous() if cs.shape[1] != ctx.P else cs, out=gout(ar, bp))
+        else:
+            K.linear_wgrad(dpred, h, out=dWp)
+            dbp = _reduce(cs, out=gout(ar, bp))
         dx, _, pg, pb, _ = K.ln_bwd(dh, x2, m, r, ctx.dn_w)
-        return dx.view(ctx.shape), None, None, None, _reduce(pg), _reduce(pb), dWp, dbp
+        return (dx.view(ctx.shape), None, None, None, _reduce(pg, out=gout(ar, dn_w)), _reduce(pb, out=gout(ar, dn_b)),
+                dWp, dbp)
 
 
 # --------------------------------------------------------- projection head
@@ -378,6 +435,8 @@ class ProjectionHeadFn(torch.autograd.Function):
                                    seed_in=spec.seed, xsum=True, step_ptr=spec.step_ptr)
         ctx.save = (x, pre, g, z, m, r)
         ctx.w = (wp, wf, lw)
+        ctx.params = (wp, bp, wf, bf, lw, lb)
+        ctx.arena = _arena()
         ctx.spec = spec
         # the step counter advances at the end of the forward: the backward
         # re-draws this forward's dropout mask from a snapshot of the step
@@ -385,19 +444,21 @@ class ProjectionHeadFn(torch.autograd.Function):
         return out
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, gout_):
         x, pre, g, z, m, r = ctx.save
         wp, wf, lw = ctx.w
         spec = ctx.spec
-        dz, _, pg, pb, _ = K.ln_bwd(gout.contiguous(), z, m, r, lw)
+        wp_, bp_, wf_, bf_, lw_, lb_ = ctx.params
+        ar = ctx.arena
+        dz, _, pg, pb, _ = K.ln_bwd(gout_.contiguous(), z, m, r, lw)
         df = K.dropout(dz, spec.p_drop, spec.seed, step_ptr=ctx.step_snap) if spec.p_drop > 0 else dz
-        dwf = K.linear_wgrad(df, g)
-        dbf = _reduce(K.rows_colsum(df))
+        dwf = K.linear_wgrad(df, g, out=gout(ar, wf_))
+        dbf = _reduce(K.rows_colsum(df), out=gout(ar, bf_))
         dpre = K.linear_dgrad(df, wf, out_dtype=torch.float32, epilogue=K.EPI_DGELU, aux=pre, resid=dz)
-        dwp = K.linear_wgrad(dpre, x)
-        dbp = _reduce(K.rows_colsum(dpre))
+        dwp = K.linear_wgrad(dpre, x, out=gout(ar, wp_))
+        dbp = _reduce(K.rows_colsum(dpre), out=gout(ar, bp_))
         dx = K.linear_dgrad(dpre, wp, out_dtype=torch.float32)
-        return dx, None, dwp, dbp, dwf, dbf, _reduce(pg), _reduce(pb)
+        return dx, None, dwp, dbp, dwf, dbf, _reduce(pg, out=gout(ar, lw_)), _reduce(pb, out=gout(ar, lb_))
 
 
 # ------------------------------------------------------------- CLIP loss

@@ -69,9 +69,19 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
     if LAUNCH_HOOK is None:
         _call("maeclip_gemm", C.byref(a), _stream())
     else:
+        ea, ec = A.element_size(), Cout.element_size()
+        # algorithmic HBM bytes of the launch: operands once, C written once
+        # (read too when beta != 0), aux read / aux_out written, fp32 residual read
+        nbytes = (M * K + N * K) * ea * batch + M * N * ec * batch * (2 if beta != 0.0 else 1)
+        if aux is not None:
+            nbytes += M * N * aux.element_size() * batch
+        if aux_out is not None:
+            nbytes += M * N * aux_out.element_size() * batch
+        if resid is not None:
+            nbytes += M * N * 4 * batch
         key = (f"M{M} N{N} K{K} {'KR'[a_layout]}{'KR'[b_layout]} epi{epilogue} "
-               f"{'bf16' if A.dtype == torch.bfloat16 else 'f32'}")
-        LAUNCH_HOOK(key, 2.0 * M * N * K * batch, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
+               f"{'bf16' if A.dtype == torch.bfloat16 else 'f32'}>{'bf16' if Cout.dtype == torch.bfloat16 else 'f32'}")
+        LAUNCH_HOOK(key, 2.0 * M * N * K * batch, nbytes, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
 
 
 def gemm_colsum_rows(M: int) -> int:

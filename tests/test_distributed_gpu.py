@@ -1,0 +1,95 @@
+"""The product's data-parallel branch on the GPU box: two ranks (two
+processes on cuda:0, gloo process group -- one MI355X, and RCCL refuses two
+ranks on one device) run mae_clip_amd.CLIPModel under
+distributed.DataParallel on B rows each; the result must equal one process
+running the same model on the 2B rows:
+  * CLIPModel.forward's world > 1 branch: embeddings all-gathered in rank
+    order, the fused CLIP loss of the gathered batch with the gradient of the
+    local rows only (grad_rows), MAE term scaled by 1/world, masks keyed by
+    the global sample index (sample_offset = rank * B);
+  * gradients written straight into the GradArena slots by the product's
+    autograd Functions and SUM-all-reduced in place (no flatten copies)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B_LOCAL = 4
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model(precision="fp32"):
+    from tests.helpers import product_config, C0
+    from mae_clip_amd.CLIP import CLIPModel
+    kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    with product_config(precision=precision, **kw):
+        torch.manual_seed(0)
+        m = CLIPModel()
+    return m.cuda().eval()
+
+
+def _batch():
+    from tests.helpers import make_batch
+    return make_batch(2 * B_LOCAL, 32, seed=3)
+
+
+def _rank(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mae_clip_amd import _lib
+        from mae_clip_amd.distributed import DataParallel
+        _lib.load()
+        m = _model()
+        dp = DataParallel(m, bucket_mb=0.5)
+        b = {k: v[rank * B_LOCAL:(rank + 1) * B_LOCAL].cuda() for k, v in _batch().items()}
+        for p in m.parameters():
+            p.grad = None
+        loss = m(b)
+        loss.backward()
+        dp.sync_gradients()
+        torch.cuda.synchronize()
+        out[rank] = dict(clip=m.last_losses["clip"].item(), mae=m.last_losses["mae"].item(),
+                         mask=m.last_mask[2].cpu(), adopted=dp.adopted, nparams=len(dp.params),
+                         nbuckets=len(dp.buckets),
+                         grads={n: p.grad.cpu() for n, p in m.named_parameters() if p.requires_grad})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_product_data_parallel_equals_full_batch(dev):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank, args=(2, _free_port(), out), nprocs=2, join=True)
+    res = [out[r] for r in range(2)]
+    m = _model()
+    full = {k: v.to(dev) for k, v in _batch().items()}
+    m(full).backward()
+    ref_clip, ref_mae = m.last_losses["clip"].item(), m.last_losses["mae"].item()
+    ref_mask = m.last_mask[2].cpu()
+    for r, o in enumerate(res):
+        assert abs(o["clip"] - ref_clip) < 1e-5 * max(1.0, abs(ref_clip)), (o["clip"], ref_clip)
+        assert torch.equal(o["mask"], ref_mask[r * B_LOCAL:(r + 1) * B_LOCAL])
+        # every trainable gradient was produced in its arena slot (no copy)
+        assert o["adopted"] == o["nparams"], (o["adopted"], o["nparams"])
+        assert o["nbuckets"] > 2
+    assert abs((res[0]["mae"] + res[1]["mae"]) / 2 - ref_mae) < 1e-5
+    for n, p in m.named_parameters():
+        if not p.requires_grad:
+            continue
+        g = p.grad.cpu()
+        sc = g.abs().max().item() + 1e-30
+        for o in res:
+            assert (o["grads"][n] - g).abs().max().item() / sc < 1e-4, n
+        assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
