@@ -25,7 +25,7 @@ from . import config as CFG
 from . import functions as Fn
 from . import kernels as K
 from .modules import (ImageEncoder, TextEncoder, ProjectionHead, MAEDecoder, WeightCache, compute_dtype,
-                      run_stack)
+                      run_stack, _require_device)
 
 
 class CLIPModel(nn.Module):
@@ -91,16 +91,14 @@ class CLIPModel(nn.Module):
 
     def forward(self, batch):
         img = batch["image"]
-        if not img.is_cuda:
-            raise RuntimeError("mae_clip_amd.CLIPModel needs the batch on a ROCm device (no CPU fallback)")
+        _require_device(img, "image batch")
         dtype = compute_dtype(self.precision)
         vit = self.image_encoder.model
         B = img.shape[0]
         world, rank = self._world()
         Fn.set_grad_arena(self.grad_arena if torch.is_grad_enabled() else None)
         sc = self.step_counter
-        if not sc.is_cuda:
-            raise RuntimeError("CLIPModel.step_counter must live on the GPU (call .to(device))")
+        _require_device(sc, "CLIPModel.step_counter (call .to(device))")
         # step-independent seed base; the kernels add step_counter * MAECLIP_STEP_MULT
         seed = (self.dropout_seed * 1000003 + rank) & 0x7FFFFFFFFFFFFFFF
         # the frozen text tower (no autograd, own bf16 weights) is independent of

@@ -303,11 +303,15 @@ def tokens_fwd(y, ids_shuffle, pos, cls, B, L_, keep):
     return x
 
 
-def tokens_bwd(dx, ids_restore, B, L_, keep, dy_dtype):
+def tokens_bwd(dx, ids_restore, B, L_, keep, dy_dtype, dpos=None, dcls=None):
     D = dx.shape[-1]
     dy = torch.empty((B * keep, D), device=dx.device, dtype=dy_dtype)
-    dpos = torch.empty((L_ + 1, D), device=dx.device, dtype=torch.float32)
-    dcls = torch.empty((D,), device=dx.device, dtype=torch.float32)
+    if dpos is None:
+        dpos = torch.empty((L_ + 1, D), device=dx.device, dtype=torch.float32)
+    if dcls is None:
+        dcls = torch.empty((D,), device=dx.device, dtype=torch.float32)
+    if dpos.shape != (L_ + 1, D) or dcls.shape != (D,) or not (dpos.is_contiguous() and dcls.is_contiguous()):
+        raise ValueError("tokens_bwd: dpos [L+1, D] / dcls [D] must be dense")
     a = L.TokensArgs(y=None, ldy=D, ids_shuffle=None, ids_restore=_ptr(ids_restore), pos=None, cls=None, x=None,
                      dx=dx.data_ptr(), dy=dy.data_ptr(), dpos=dpos.data_ptr(), dcls=dcls.data_ptr(),
                      B=B, L=L_, keep=keep, D=D, dtype=_dt(dy))
@@ -450,9 +454,12 @@ class ReduceBatch:
     def __init__(self):
         self.items = []
 
-    def add(self, partial, scale=1.0):
+    def add(self, partial, scale=1.0, out=None):
         P, N = partial.shape
-        out = torch.empty((N,), device=partial.device, dtype=torch.float32)
+        if out is None:
+            out = torch.empty((N,), device=partial.device, dtype=torch.float32)
+        elif out.numel() != N or not out.is_contiguous():
+            raise ValueError("ReduceBatch.add: out must be a dense [N] tensor")
         self.items.append((partial, out, scale))
         return out
 

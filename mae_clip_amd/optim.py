@@ -63,8 +63,7 @@ class AdamW(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if not p.is_cuda:
-                    raise RuntimeError("mae_clip_amd.optim.AdamW needs ROCm device parameters")
+                K._dev(p)   # ROCm device parameters only (raises otherwise)
                 st = self.state[p]
                 if not st:
                     st["step"] = 0
