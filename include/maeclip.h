@@ -322,8 +322,10 @@ int32_t maeclip_tokens_fwd(const maeclip_tokens_args* args, void* stream);
 int32_t maeclip_tokens_bwd(const maeclip_tokens_args* args, void* stream);
 
 /* HF ViTMAEDecoder mask-token append + unshuffle + pos (modeling_vit_mae.py:548-566).
- * fwd: y f32 [B, 1+keep, ldy] -> out f32 [B, 1+L, D]. bwd: dout f32 -> dy
- * (dtype) [B, 1+keep, ldy], dmask_partial / colsum_partial f32 [B, D]. */
+ * fwd: y f32 [B, 1+keep, ldy] -> out f32 [B, 1+L, D]. bwd (reads ids_restore):
+ * dout f32 -> dy (dtype) [B, 1+keep, ldy]; dmask_partial / colsum_partial f32
+ * [maeclip_unshuffle_bwd_partial_rows(B), D] (column-reduce them: mask_token
+ * and decoder_embed bias gradients). D % 4 == 0, D <= 1024. */
 typedef struct {
   const float* y;
   int64_t ldy;
@@ -340,12 +342,15 @@ typedef struct {
 } maeclip_unshuffle_args;
 int32_t maeclip_unshuffle_fwd(const maeclip_unshuffle_args* args, void* stream);
 int32_t maeclip_unshuffle_bwd(const maeclip_unshuffle_args* args, void* stream);
+int32_t maeclip_unshuffle_bwd_partial_rows(int32_t B);
 
 /* MAE reconstruction loss (modeling_vit_mae.py:706-745 patchify, :852-859).
  * pred: decoder output rows [B, 1+L, ldp] (row 0 = cls, ignored); targets are
- * patchified from img on the fly. fwd: row_loss [B*L] = mask * mean_k diff^2
- * (sum / mask_count outside). bwd: dpred [B, 1+L, lddp] = grad_out[0] *
- * loss_scale * 2 diff mask / (P * mask_count); colsum_partial [B, P] optional. */
+ * patchified from img on the fly (only for masked patches). fwd: row_loss [B*L]
+ * = mask * mean_k diff^2 (sum / mask_count outside). bwd: dpred [B, 1+L, lddp]
+ * = grad_out[0] * loss_scale * 2 diff mask / (P * mask_count) (columns
+ * [P, lddp) zeroed); colsum_partial [maeclip_mae_loss_bwd_partial_rows(B, L)][P]
+ * optional. P = C*p*p <= 1024, P % 4 == 0. */
 typedef struct {
   const void* pred;
   int64_t ldp;
@@ -361,6 +366,7 @@ typedef struct {
 } maeclip_mae_loss_args;
 int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* args, void* stream);
 int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* args, void* stream);
+int32_t maeclip_mae_loss_bwd_partial_rows(int32_t B, int32_t L);
 
 /* ------------------------------------------------------------- CLIP loss
  * CLIPModel.forward loss (CLIP.py:34-43) + cross_entropy (CLIP.py:46-52), fp32,

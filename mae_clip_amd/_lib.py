@@ -153,8 +153,10 @@ _SIGS = {
     "maeclip_tokens_bwd": (c_i32, [C.POINTER(TokensArgs), c_vp]),
     "maeclip_unshuffle_fwd": (c_i32, [C.POINTER(UnshuffleArgs), c_vp]),
     "maeclip_unshuffle_bwd": (c_i32, [C.POINTER(UnshuffleArgs), c_vp]),
+    "maeclip_unshuffle_bwd_partial_rows": (c_i32, [c_i32]),
     "maeclip_mae_loss_fwd": (c_i32, [C.POINTER(MaeLossArgs), c_vp]),
     "maeclip_mae_loss_bwd": (c_i32, [C.POINTER(MaeLossArgs), c_vp]),
+    "maeclip_mae_loss_bwd_partial_rows": (c_i32, [c_i32, c_i32]),
     "maeclip_clip_loss_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "maeclip_clip_loss": (c_i32, [C.POINTER(ClipArgs), c_vp]),
     "maeclip_counter_add": (c_i32, [c_vp, c_i64, c_vp]),

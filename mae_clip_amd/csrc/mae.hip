@@ -119,26 +119,55 @@ __global__ void __launch_bounds__(NTH) tokens_bwd_dy_kernel(const maeclip_tokens
   st4<YT>((YT*)a.dy + r * a.ldy + d, v);
 }
 // dpos[1+l] = sum_b [kept] dx[b,1+restore[b,l]] ; dpos[0] = dcls = sum_b dx[b,0]
+// One workgroup per (position, 256-column chunk): wave w sums the samples
+// b = w, w+4, ... (16-B loads, four rows in flight per lane), the four wave
+// partials are added in a fixed order through LDS (deterministic).
 __global__ void __launch_bounds__(NTH) tokens_bwd_pos_kernel(const maeclip_tokens_args a) {
-  const int pr = blockIdx.y;  // 0..L
-  const int d = blockIdx.x * NTH + threadIdx.x;
-  if (d >= a.D) return;
+  __shared__ v4f red[NTH / 64][64];
+  const int pr = blockIdx.x;  // 0..L
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = (blockIdx.y * 64 + lane) * 4;
   const int nt = a.keep + 1;
-  float s = 0.f;
-  for (int b = 0; b < a.B; ++b) {
-    int t;
-    if (pr == 0) {
-      t = 0;
-    } else {
-      const int l = pr - 1;
-      const int r = a.ids_restore ? a.ids_restore[(int64_t)b * a.L + l] : l;
-      if (r >= a.keep) continue;
-      t = 1 + r;
+  v4f acc = {0.f, 0.f, 0.f, 0.f};
+  if (d < a.D) {
+    int b = wave;
+    for (; b + 12 < a.B; b += 16) {
+      v4f v[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int bb = b + 4 * u;
+        int t = 0;
+        ok[u] = true;
+        if (pr > 0) {
+          const int r = a.ids_restore ? a.ids_restore[(int64_t)bb * a.L + pr - 1] : pr - 1;
+          ok[u] = r < a.keep;
+          t = 1 + (ok[u] ? r : 0);
+        }
+        v[u] = *(const v4f*)(a.dx + ((int64_t)bb * nt + t) * a.D + d);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) acc += v[u];
     }
-    s += a.dx[((int64_t)b * nt + t) * a.D + d];
+    for (; b < a.B; b += 4) {
+      int t = 0;
+      bool ok = true;
+      if (pr > 0) {
+        const int r = a.ids_restore ? a.ids_restore[(int64_t)b * a.L + pr - 1] : pr - 1;
+        ok = r < a.keep;
+        t = 1 + (ok ? r : 0);
+      }
+      if (ok) acc += *(const v4f*)(a.dx + ((int64_t)b * nt + t) * a.D + d);
+    }
   }
-  a.dpos[(int64_t)pr * a.D + d] = s;
-  if (pr == 0 && a.dcls) a.dcls[d] = s;
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && d < a.D) {
+    const v4f sum = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    *(v4f*)(a.dpos + (int64_t)pr * a.D + d) = sum;
+    if (pr == 0 && a.dcls) *(v4f*)(a.dcls + d) = sum;
+  }
 }
 
 // decoder input: out[b,0] = y[b,0] + pos[0]; out[b,1+l] = (restore<keep ? y[b,1+restore] : mask_token) + pos[1+l]
@@ -158,129 +187,201 @@ __global__ void __launch_bounds__(NTH) unshuffle_fwd_kernel(const maeclip_unshuf
   *(v4f*)(a.out + row * a.D + d) = v;
 }
 
-// dy[b,0] = dout[b,0]; dy[b,1+j] = dout[b,1+shuffle[b,j]];  partials per sample:
-// dmask[b] = sum_{j>=keep} dout[b,1+shuffle[b,j]],  colsum[b] = sum_t dy[b,t]
+// dy[b,0] = dout[b,0]; dy[b,1+r] = dout[b,1+l] for r = restore[b,l] < keep;
+// partials: dmask = sum of dout rows of masked positions, colsum = sum of the
+// dy rows. Workgroup (b, q) reads rows t = q, q+UQ, ... of sample b in natural
+// order (coalesced 16-B loads; rows scattered only on the dy write side), wave
+// w takes every 4th of them, lane = 4-column chunk; partial row b*UQ + q.
+constexpr int UQ = 4;   // workgroups per sample
 template <typename YT>
 __global__ void __launch_bounds__(NTH) unshuffle_bwd_kernel(const maeclip_unshuffle_args a) {
-  const int b = blockIdx.y;
-  const int d = (blockIdx.x * NTH + threadIdx.x);
-  if (d >= a.D) return;
-  const float* base = a.dout + (int64_t)b * (a.L + 1) * a.D + d;
-  YT* dyb = (YT*)a.dy + (int64_t)b * (a.keep + 1) * a.ldy + d;
-  float v0 = base[0];
-  st_from_f<YT>(dyb, v0);
-  float cs = v0, dm = 0.f;
-  for (int j = 0; j < a.L; ++j) {
-    const int l = a.ids_shuffle[(int64_t)b * a.L + j];
-    const float v = base[(int64_t)(1 + l) * a.D];
-    if (j < a.keep) {
-      st_from_f<YT>(dyb + (int64_t)(1 + j) * a.ldy, v);
-      cs += v;
-    } else {
-      dm += v;
-    }
-  }
-  if (a.dmask_partial) a.dmask_partial[(int64_t)b * a.D + d] = dm;
-  if (a.colsum_partial) a.colsum_partial[(int64_t)b * a.D + d] = cs;
-}
-
-constexpr int MAXK = 16;  // elements per lane -> p*p*C <= 1024
-
-// target element k = (ky*p + kx)*C + c of patch l of sample b
-__device__ __forceinline__ float target_px(const maeclip_mae_loss_args& a, int b, int l, int k) {
-  const int C = a.C, p = a.p, w = a.S / p;
-  const int c = k % C, pix = k / C;
-  const int ky = pix / p, kx = pix % p;
-  const int py = l / w, px = l % w;
-  return a.img[(((int64_t)b * C + c) * a.S + py * p + ky) * a.S + px * p + kx];
-}
-
-template <typename PT>
-__device__ __forceinline__ void patch_diff(const maeclip_mae_loss_args& a, int b, int l, int lane, float (&df)[MAXK]) {
-  const int P = a.C * a.p * a.p;
-  const PT* pred = (const PT*)a.pred + ((int64_t)b * (a.L + 1) + 1 + l) * a.ldp;
-  float t[MAXK];
+  constexpr int MC = 4;   // <= 4 x 64 four-column chunks: D <= 1024
+  __shared__ v4f red[2][NTH / 64][MC * 64];
+  const int b = blockIdx.x, q = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nc = a.D / 4;
+  v4f cs[MC], dm[MC];
 #pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const int k = lane + 64 * i;
-    t[i] = k < P ? target_px(a, b, l, k) : 0.f;
-  }
-  if (a.norm_pix) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i) s += t[i];
-    const float mean = wave_sum(s) / P;
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i)
-      if (lane + 64 * i < P) ss += (t[i] - mean) * (t[i] - mean);
-    const float var = wave_sum(ss) / (P - 1);
-    const float inv = 1.f / sqrtf(var + 1.0e-6f);
-#pragma unroll
-    for (int i = 0; i < MAXK; ++i) t[i] = (t[i] - mean) * inv;
-  }
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const int k = lane + 64 * i;
-    df[i] = k < P ? ld_as_f<PT>(pred + k) - t[i] : 0.f;
-  }
-}
-
-template <typename PT>
-__global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_loss_args a) {
-  const int64_t wid = (int64_t)blockIdx.x * (NTH / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (wid >= (int64_t)a.B * a.L) return;
-  const int b = (int)(wid / a.L), l = (int)(wid % a.L);
-  const float mk = a.mask[wid];
-  float df[MAXK];
-  patch_diff<PT>(a, b, l, lane, df);
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) s += df[i] * df[i];
-  s = wave_sum(s);
-  if (lane == 0) a.row_loss[wid] = mk * s / (float)(a.C * a.p * a.p);
-}
-
-// one workgroup per sample; waves stride over its 1+L rows (row 0 = cls -> 0)
-template <typename PT>
-__global__ void __launch_bounds__(NTH) mae_loss_bwd_kernel(const maeclip_mae_loss_args a) {
-  __shared__ float red[NTH / 64][MAXK * 64];
-  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int P = a.C * a.p * a.p;
-  const float gscale = (a.grad_out ? a.grad_out[0] : 1.f) * a.loss_scale * 2.f / ((float)P * a.mask_count);
-  float cs[MAXK];
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) cs[i] = 0.f;
-  for (int r = wave; r < a.L + 1; r += NTH / 64) {
-    PT* drow = (PT*)a.dpred + ((int64_t)b * (a.L + 1) + r) * a.lddp;
-    float df[MAXK];
-    float mk = 0.f;
-    if (r > 0) {
-      mk = a.mask[(int64_t)b * a.L + r - 1];
-      patch_diff<PT>(a, b, r - 1, lane, df);
+  for (int i = 0; i < MC; ++i) cs[i] = dm[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  const float* base = a.dout + (int64_t)b * (a.L + 1) * a.D;
+  YT* dyb = (YT*)a.dy + (int64_t)b * (a.keep + 1) * a.ldy;
+  for (int t = q + UQ * wave; t < a.L + 1; t += UQ * (NTH / 64)) {
+    int r = 0;
+    bool kept = true;
+    if (t > 0) {
+      r = a.ids_restore[(int64_t)b * a.L + t - 1];
+      kept = r < a.keep;
+      r += 1;
     }
 #pragma unroll
-    for (int i = 0; i < MAXK; ++i) {
-      const int k = lane + 64 * i;
-      if (k < P) {
-        const float g = (r > 0) ? gscale * mk * df[i] : 0.f;
-        st_from_f<PT>(drow + k, g);
-        cs[i] += g;
+    for (int i = 0; i < MC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        const v4f v = *(const v4f*)(base + (int64_t)t * a.D + 4 * c);
+        if (kept) {
+          st4<YT>(dyb + (int64_t)r * a.ldy + 4 * c, v);
+          cs[i] += v;
+        } else {
+          dm[i] += v;
+        }
       }
     }
   }
-  if (a.colsum_partial) {
 #pragma unroll
-    for (int i = 0; i < MAXK; ++i) red[wave][lane + 64 * i] = cs[i];
-    __syncthreads();
-    for (int k = threadIdx.x; k < P; k += NTH) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < NTH / 64; ++w) s += red[w][k];
-      a.colsum_partial[(int64_t)b * P + k] = s;
-    }
+  for (int i = 0; i < MC; ++i) {
+    red[0][wave][lane + 64 * i] = cs[i];
+    red[1][wave][lane + 64 * i] = dm[i];
   }
+  __syncthreads();
+  const int64_t prow = (int64_t)b * UQ + q;
+  for (int c = threadIdx.x; c < nc; c += NTH) {
+    const v4f s0 = ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
+    const v4f s1 = ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+    if (a.colsum_partial) *(v4f*)(a.colsum_partial + prow * a.D + 4 * c) = s0;
+    if (a.dmask_partial) *(v4f*)(a.dmask_partial + prow * a.D + 4 * c) = s1;
+  }
+}
+
+constexpr int PMAX = 1024;   // p*p*C <= 1024 (ViT-B/16: 768, ViT-L/14: 588)
+
+// Target pixels of patch l of sample b into the wave's LDS row tg[P] in the
+// HF patchify order k = (ky*p + kx)*C + c (modeling_vit_mae.py:739). The image
+// is read in its own (c, ky, kx) order -- VW-float vectors along kx, so
+// consecutive lanes read consecutive bytes of one pixel row -- and the
+// channel interleave happens on the LDS write.
+template <int VW>
+__device__ __forceinline__ void load_target(const maeclip_mae_loss_args& a, int b, int l, float* tg, int lane) {
+  const int C = a.C, p = a.p, w = a.S / p;
+  const int py = l / w, px = l % w;
+  const int vpr = p / VW, nv = C * p * vpr;
+  const float* img = a.img + (int64_t)b * C * a.S * a.S + (int64_t)(py * p) * a.S + px * p;
+  for (int v = lane; v < nv; v += 64) {
+    const int r = v / vpr, kx = (v - r * vpr) * VW;
+    const int c = r / p, ky = r - c * p;
+    const float* src = img + ((int64_t)c * a.S + ky) * a.S + kx;
+    float t[VW];
+    if constexpr (VW == 4) {
+      const v4f x = *(const v4f*)src;
+      t[0] = x[0]; t[1] = x[1]; t[2] = x[2]; t[3] = x[3];
+    } else if constexpr (VW == 2) {
+      const float2 x = *(const float2*)src;
+      t[0] = x.x; t[1] = x.y;
+    } else {
+      t[0] = src[0];
+    }
+#pragma unroll
+    for (int e = 0; e < VW; ++e) tg[(ky * p + kx + e) * C + c] = t[e];
+  }
+}
+
+// norm_pix_loss: targets -> (t - mean) / sqrt(var + 1e-6), unbiased var (HF)
+__device__ __forceinline__ void norm_target(float* tg, int P, int lane) {
+  float s = 0.f;
+  for (int k = lane; k < P; k += 64) s += tg[k];
+  const float mean = wave_sum(s) / (float)P;
+  float ss = 0.f;
+  for (int k = lane; k < P; k += 64) {
+    const float d = tg[k] - mean;
+    ss += d * d;
+  }
+  const float inv = 1.f / sqrtf(wave_sum(ss) / (float)(P - 1) + 1.0e-6f);
+  for (int k = lane; k < P; k += 64) tg[k] = (tg[k] - mean) * inv;
+}
+
+template <int VW>
+__device__ __forceinline__ void load_target_any(const maeclip_mae_loss_args& a, int b, int l, float* tg, int lane) {
+  load_target<VW>(a, b, l, tg, lane);
+  if (a.norm_pix) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    norm_target(tg, a.C * a.p * a.p, lane);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per patch (b, l); only masked patches (mask 1) read anything.
+template <typename PT, int VW>
+__global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_loss_args a) {
+  __shared__ float tgs[NTH / 64][PMAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t wid = (int64_t)blockIdx.x * (NTH / 64) + wave;
+  if (wid >= (int64_t)a.B * a.L) return;
+  const float mk = a.mask[wid];
+  if (mk == 0.f) {
+    if (lane == 0) a.row_loss[wid] = 0.f;
+    return;
+  }
+  const int b = (int)(wid / a.L), l = (int)(wid % a.L);
+  const int P = a.C * a.p * a.p;
+  float* tg = tgs[wave];
+  load_target_any<VW>(a, b, l, tg, lane);
+  const PT* pred = (const PT*)a.pred + ((int64_t)b * (a.L + 1) + 1 + l) * a.ldp;
+  float s = 0.f;
+  for (int k = 4 * lane; k < P; k += 256) {
+    const v4f pv = ld4<PT>(pred + k);
+    const v4f tv = *(const v4f*)(tg + k);
+    const v4f d = pv - tv;
+    s += d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3];
+  }
+  s = wave_sum(s);
+  if (lane == 0) a.row_loss[wid] = mk * s / (float)P;
+}
+
+// dpred rows of a sample: workgroup (b, chunk of RB = 16 rows of 1+L), wave w
+// takes rows r0 + w + 4i; row 0 (cls) and unmasked rows are written as zeros
+// without reading. Pad columns [P, lddp) are zeroed. Per-workgroup column sums
+// (decoder_pred bias gradient) -> colsum_partial[b * nchunk + chunk][P].
+constexpr int RB = 16;
+template <typename PT, int VW>
+__global__ void __launch_bounds__(NTH) mae_loss_bwd_kernel(const maeclip_mae_loss_args a) {
+  __shared__ float tgs[NTH / 64][PMAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x, chunk = blockIdx.y;
+  const int P = a.C * a.p * a.p;
+  const float gscale = (a.grad_out ? a.grad_out[0] : 1.f) * a.loss_scale * 2.f / ((float)P * a.mask_count);
+  v4f cs[PMAX / 256];
+#pragma unroll
+  for (int i = 0; i < PMAX / 256; ++i) cs[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  float* tg = tgs[wave];
+  for (int rr = wave; rr < RB; rr += NTH / 64) {
+    const int r = chunk * RB + rr;
+    if (r > a.L) break;
+    PT* drow = (PT*)a.dpred + ((int64_t)b * (a.L + 1) + r) * a.lddp;
+    const float mk = r > 0 ? a.mask[(int64_t)b * a.L + r - 1] : 0.f;
+    if (mk == 0.f) {
+      for (int k = 4 * lane; k < (int)a.lddp; k += 256) st4<PT>(drow + k, v4f{0.f, 0.f, 0.f, 0.f});
+      continue;
+    }
+    const PT* prow = (const PT*)a.pred + ((int64_t)b * (a.L + 1) + r) * a.ldp;
+    load_target_any<VW>(a, b, r - 1, tg, lane);
+    const float g = gscale * mk;
+#pragma unroll
+    for (int i = 0; i < PMAX / 256; ++i) {
+      const int k = 4 * lane + 256 * i;
+      if (k < P) {
+        const v4f d = (ld4<PT>(prow + k) - *(const v4f*)(tg + k)) * g;
+        st4<PT>(drow + k, d);
+        cs[i] += d;
+      } else if (k < (int)a.lddp) {
+        st4<PT>(drow + k, v4f{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+    // the next row's target overwrites tg: every lane's reads of it are done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (!a.colsum_partial) return;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PMAX / 256; ++i) *(v4f*)(tg + 4 * lane + 256 * i) = cs[i];
+  __syncthreads();
+  float* prow = a.colsum_partial + ((int64_t)b * gridDim.y + chunk) * P;
+  for (int k = threadIdx.x; k < P; k += NTH)
+    prow[k] = ((tgs[0][k] + tgs[1][k]) + tgs[2][k]) + tgs[3][k];
 }
 
 }  // namespace
@@ -324,7 +425,9 @@ extern "C" int32_t maeclip_tokens_bwd(const maeclip_tokens_args* a, void* stream
     else hipLaunchKernelGGL((tokens_bwd_dy_kernel<float>), grid, dim3(NTH), 0, s, *a);
     MC_CHECK_LAUNCH("maeclip_tokens_bwd(dy)");
   }
-  dim3 g2((unsigned)((a->D + NTH - 1) / NTH), (unsigned)(a->L + 1));
+  MC_CHECK_ARG(((uintptr_t)a->dx & 15) == 0 && ((uintptr_t)a->dpos & 15) == 0 && (!a->dcls || ((uintptr_t)a->dcls & 15) == 0),
+               "maeclip_tokens_bwd: dx / dpos / dcls must be 16-byte aligned");
+  dim3 g2((unsigned)(a->L + 1), (unsigned)((a->D / 4 + 63) / 64));
   hipLaunchKernelGGL(tokens_bwd_pos_kernel, g2, dim3(NTH), 0, s, *a);
   MC_CHECK_LAUNCH("maeclip_tokens_bwd(pos)");
   return 0;
@@ -340,31 +443,66 @@ extern "C" int32_t maeclip_unshuffle_fwd(const maeclip_unshuffle_args* a, void* 
 }
 
 extern "C" int32_t maeclip_unshuffle_bwd(const maeclip_unshuffle_args* a, void* stream) {
-  MC_CHECK_ARG(a && a->dout && a->ids_shuffle && a->dy, "maeclip_unshuffle_bwd: bad args");
-  dim3 grid((unsigned)((a->D + NTH - 1) / NTH), (unsigned)a->B);
+  MC_CHECK_ARG(a && a->dout && a->ids_restore && a->dy, "maeclip_unshuffle_bwd: bad args");
+  MC_CHECK_ARG(a->D % 4 == 0 && a->D <= 1024 && a->ldy % 4 == 0 && ((uintptr_t)a->dout & 15) == 0 &&
+                   ((uintptr_t)a->dy & 7) == 0,
+               "maeclip_unshuffle_bwd: D must be a multiple of 4 (<= 1024), rows aligned");
+  dim3 grid((unsigned)a->B, UQ);
   if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((unshuffle_bwd_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
   else hipLaunchKernelGGL((unshuffle_bwd_kernel<float>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
   MC_CHECK_LAUNCH("maeclip_unshuffle_bwd");
   return 0;
 }
 
+extern "C" int32_t maeclip_unshuffle_bwd_partial_rows(int32_t B) { return B * UQ; }
+
+namespace {
+int check_loss(const maeclip_mae_loss_args* a, bool bwd) {
+  MC_CHECK_ARG(a && a->pred && a->img && a->mask, "maeclip_mae_loss: null pointer");
+  const int P = a->C * a->p * a->p;
+  MC_CHECK_ARG(P <= PMAX && P % 4 == 0 && a->ldp % 4 == 0 && a->ldp >= P && a->S % a->p == 0,
+               "maeclip_mae_loss: p*p*C must be a multiple of 4, <= %d", PMAX);
+  MC_CHECK_ARG(((uintptr_t)a->img & 15) == 0 && ((uintptr_t)a->pred & 7) == 0 && a->S % 4 == 0,
+               "maeclip_mae_loss: misaligned image / pred");
+  if (bwd) MC_CHECK_ARG(a->dpred && a->lddp % 4 == 0 && a->lddp >= P && a->mask_count > 0.f,
+                        "maeclip_mae_loss_bwd: bad dpred / mask_count");
+  else MC_CHECK_ARG(a->row_loss != nullptr, "maeclip_mae_loss_fwd: null row_loss");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int32_t maeclip_mae_loss_bwd_partial_rows(int32_t B, int32_t L) { return B * ((L + 1 + RB - 1) / RB); }
+
 extern "C" int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* a, void* stream) {
-  MC_CHECK_ARG(a && a->pred && a->img && a->mask && a->row_loss, "maeclip_mae_loss_fwd: null pointer");
-  MC_CHECK_ARG(a->C * a->p * a->p <= MAXK * 64, "maeclip_mae_loss_fwd: patch too large");
+  if (int e = check_loss(a, false)) return e;
   const int64_t nw = (int64_t)a->B * a->L;
   dim3 grid((unsigned)((nw + 3) / 4));
-  if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((mae_loss_fwd_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
-  else hipLaunchKernelGGL((mae_loss_fwd_kernel<float>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
+  hipStream_t s = (hipStream_t)stream;
+  const int vw = a->p % 4 == 0 ? 4 : (a->p % 2 == 0 ? 2 : 1);
+#define FWD(PT, VW) hipLaunchKernelGGL((mae_loss_fwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a)
+  if (a->dtype == MAECLIP_BF16) {
+    if (vw == 4) FWD(bf16_t, 4); else if (vw == 2) FWD(bf16_t, 2); else FWD(bf16_t, 1);
+  } else {
+    if (vw == 4) FWD(float, 4); else if (vw == 2) FWD(float, 2); else FWD(float, 1);
+  }
+#undef FWD
   MC_CHECK_LAUNCH("maeclip_mae_loss_fwd");
   return 0;
 }
 
 extern "C" int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* a, void* stream) {
-  MC_CHECK_ARG(a && a->pred && a->img && a->mask && a->dpred, "maeclip_mae_loss_bwd: null pointer");
-  MC_CHECK_ARG(a->C * a->p * a->p <= MAXK * 64 && a->mask_count > 0.f, "maeclip_mae_loss_bwd: bad sizes");
-  dim3 grid((unsigned)a->B);
-  if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((mae_loss_bwd_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
-  else hipLaunchKernelGGL((mae_loss_bwd_kernel<float>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
+  if (int e = check_loss(a, true)) return e;
+  dim3 grid((unsigned)a->B, (unsigned)((a->L + 1 + RB - 1) / RB));
+  hipStream_t s = (hipStream_t)stream;
+  const int vw = a->p % 4 == 0 ? 4 : (a->p % 2 == 0 ? 2 : 1);
+#define BWD(PT, VW) hipLaunchKernelGGL((mae_loss_bwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a)
+  if (a->dtype == MAECLIP_BF16) {
+    if (vw == 4) BWD(bf16_t, 4); else if (vw == 2) BWD(bf16_t, 2); else BWD(bf16_t, 1);
+  } else {
+    if (vw == 4) BWD(float, 4); else if (vw == 2) BWD(float, 2); else BWD(float, 1);
+  }
+#undef BWD
   MC_CHECK_LAUNCH("maeclip_mae_loss_bwd");
   return 0;
 }

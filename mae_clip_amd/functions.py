@@ -343,7 +343,7 @@ class DecoderEmbedFn(torch.autograd.Function):
         y = K.linear_fwd(latent, spec.w_T, b, out_dtype=torch.float32)
         xd = K.unshuffle_fwd(y, ids_restore, mask_token.view(-1), pos.view(-1, pos.shape[-1]), spec.B, spec.L,
                              spec.keep)
-        ctx.save = (latent, ids_shuffle)
+        ctx.save = (latent, ids_restore)
         ctx.spec = spec
         ctx.params = (w, b, mask_token)
         ctx.arena = _arena()
@@ -352,8 +352,8 @@ class DecoderEmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gxd):
         spec = ctx.spec
-        latent, ids_shuffle = ctx.save
-        dy, dmask_part, cs = K.unshuffle_bwd(gxd.contiguous(), ids_shuffle, spec.B, spec.L, spec.keep, spec.dtype)
+        latent, ids_restore = ctx.save
+        dy, dmask_part, cs = K.unshuffle_bwd(gxd.contiguous(), ids_restore, spec.B, spec.L, spec.keep, spec.dtype)
         w, b, mask_token = ctx.params
         ar = ctx.arena
         dlatent = K.linear_dgrad(dy, spec.w_T)

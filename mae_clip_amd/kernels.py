@@ -329,13 +329,14 @@ def unshuffle_fwd(y, ids_restore, mask_token, pos, B, L_, keep):
     return out
 
 
-def unshuffle_bwd(dout, ids_shuffle, B, L_, keep, dy_dtype):
+def unshuffle_bwd(dout, ids_restore, B, L_, keep, dy_dtype):
     D = dout.shape[-1]
     dy = torch.empty((B * (keep + 1), D), device=dout.device, dtype=dy_dtype)
-    dmask = torch.empty((B, D), device=dout.device, dtype=torch.float32)
-    cs = torch.empty((B, D), device=dout.device, dtype=torch.float32)
-    a = L.UnshuffleArgs(y=None, ldy=D, ids_shuffle=ids_shuffle.data_ptr(), ids_restore=None, mask_token=None, pos=None,
-                        out=None, dout=dout.data_ptr(), dy=dy.data_ptr(), dmask_partial=dmask.data_ptr(),
+    G = int(L.lib().maeclip_unshuffle_bwd_partial_rows(B))
+    dmask = torch.empty((G, D), device=dout.device, dtype=torch.float32)
+    cs = torch.empty((G, D), device=dout.device, dtype=torch.float32)
+    a = L.UnshuffleArgs(y=None, ldy=D, ids_shuffle=None, ids_restore=ids_restore.data_ptr(), mask_token=None,
+                        pos=None, out=None, dout=dout.data_ptr(), dy=dy.data_ptr(), dmask_partial=dmask.data_ptr(),
                         colsum_partial=cs.data_ptr(), B=B, L=L_, keep=keep, D=D, dtype=_dt(dy))
     _call("maeclip_unshuffle_bwd", C.byref(a), _stream())
     return dy, dmask, cs
@@ -357,10 +358,11 @@ def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=
     B, Cc, S, _ = img.shape
     L_ = mask.shape[1]
     P = Cc * p * p
-    # padded pred rows (decoder_pred N rounded up for the GEMM): the pad columns
-    # of dpred must be zeros (they meet the zero rows of the padded weight)
-    dpred = torch.empty_like(pred) if pred.shape[1] == P else torch.zeros_like(pred)
-    cs = torch.empty((B, P), device=img.device, dtype=torch.float32)
+    # padded pred rows (decoder_pred N rounded up for the GEMM): the kernel
+    # zeroes dpred's pad columns (they meet the zero rows of the padded weight)
+    dpred = torch.empty_like(pred)
+    G = int(L.lib().maeclip_mae_loss_bwd_partial_rows(B, L_))
+    cs = torch.empty((G, P), device=img.device, dtype=torch.float32)
     a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
                       row_loss=None, dpred=dpred.data_ptr(), lddp=dpred.stride(0), grad_out=_ptr(grad_out),
                       colsum_partial=cs.data_ptr(), loss_scale=loss_scale, mask_count=float(mask_count),

@@ -425,3 +425,75 @@ def test_retrieval_normalize_similarity_topk(dev, QNk):
         order = sorted(range(N), key=lambda i: (-sc[q, i].item(), i))[:k]
         assert idx[q].tolist() == order
         assert torch.equal(vals[q].cpu(), s[q].cpu()[idx[q].cpu()])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", [(4, 224, 16, False), (3, 224, 16, True), (2, 336, 14, False), (2, 32, 8, True)])
+def test_mae_loss_kernels_vs_torch(dev, dtype, cfg):
+    """HF ViTMAE forward_loss (modeling_vit_mae.py:852-859) over patchify
+    (:706-745) on the fused kernels: per-patch loss rows and the gradient of
+    the scaled mean, incl. norm_pix and the padded pred rows of patch 14
+    (P = 588 in a 640-wide row; dpred pad columns must come back zero)."""
+    from oracle.ref_model import patchify
+    B, S, p, norm_pix = cfg
+    L_ = (S // p) ** 2
+    P = 3 * p * p
+    ldp = (P + 63) // 64 * 64
+    keep = L_ // 4
+    img = _rand((B, 3, S, S), torch.float32, dev, seed=51)
+    pred_full = _rand((B * (L_ + 1), ldp), dtype, dev, seed=52)
+    _, _, mask, _ = K.mask_ids(B, L_, keep, seed=2, step=7, sample_offset=0, device=dev)
+    row = K.mae_loss_fwd(pred_full, img, mask, p, norm_pix)
+    tgt = patchify(img.double().cpu(), p)
+    if norm_pix:
+        mean = tgt.mean(-1, keepdim=True)
+        var = tgt.var(-1, keepdim=True)
+        tgt = (tgt - mean) / (var + 1e-6) ** 0.5
+    pr = pred_full.double().cpu().view(B, L_ + 1, ldp)[:, 1:, :P].clone().requires_grad_(True)
+    ref_row = ((pr - tgt) ** 2).mean(-1) * mask.double().cpu()
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    assert (row.double().cpu().view(B, L_) - ref_row).abs().max().item() < tol * ref_row.abs().max().item() + 1e-6
+    mc = float(mask.sum().item())
+    gl = torch.tensor(0.7, device=dev)
+    dpred, cs = K.mae_loss_bwd(pred_full, img, mask, p, norm_pix, gl, mc, loss_scale=0.5)
+    (ref_row.sum() / mc * 0.5 * 0.7).backward()
+    d = dpred.double().cpu().view(B, L_ + 1, ldp)
+    gs = pr.grad.abs().max().item()
+    tolg = 1e-5 if dtype == torch.float32 else 1e-2
+    assert (d[:, 1:, :P] - pr.grad).abs().max().item() < tolg * gs
+    assert torch.count_nonzero(d[:, 0]) == 0 and torch.count_nonzero(d[:, :, P:]) == 0
+    assert (cs.double().cpu().sum(0) - d[:, :, :P].sum((0, 1))).abs().max().item() < 1e-4 * gs * L_
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
+    """timm _pos_embed / PatchEmbed backward on the visible tokens and the HF
+    decoder unshuffle backward (modeling_vit_mae.py:548-566): gathered rows
+    exact, position / mask-token / bias partial sums vs fp64."""
+    B, L_, keep, D, Dd = 16, 196, 49, 768, 512
+    ids_s, ids_r, mask, _ = K.mask_ids(B, L_, keep, seed=2, step=1, sample_offset=0, device=dev)
+    dx = _rand((B, keep + 1, D), torch.float32, dev, seed=61)
+    dy, dpos, dcls = K.tokens_bwd(dx, ids_r, B, L_, keep, dtype)
+    assert torch.equal(dy.float().view(B, keep, D), dx[:, 1:].to(dtype).float())
+    ref = torch.zeros(L_ + 1, D, dtype=torch.float64)
+    x64 = dx.double().cpu()
+    ref[0] = x64[:, 0].sum(0)
+    s = ids_s.cpu().long()
+    for b in range(B):
+        ref[1 + s[b, :keep]] += x64[b, 1:]
+    assert (dpos.double().cpu() - ref).abs().max().item() < 1e-4
+    assert torch.equal(dcls, dpos[0])
+    dout = _rand((B, L_ + 1, Dd), torch.float32, dev, seed=62)
+    dy2, dmask, cs = K.unshuffle_bwd(dout, ids_r, B, L_, keep, dtype)
+    o64 = dout.double().cpu()
+    r = ids_r.cpu().long()
+    ref_dy = torch.zeros(B, keep + 1, Dd, dtype=torch.float64)
+    ref_dy[:, 0] = o64[:, 0]
+    ref_dm = torch.zeros(Dd, dtype=torch.float64)
+    for b in range(B):
+        kept = r[b] < keep
+        ref_dy[b, 1 + r[b][kept]] = o64[b, 1:][kept]
+        ref_dm += o64[b, 1:][~kept].sum(0)
+    assert torch.equal(dy2.float().view(B, keep + 1, Dd), ref_dy.float().to(dtype).float().to(dev).cpu())
+    assert (dmask.double().cpu().sum(0) - ref_dm).abs().max().item() < 1e-3
+    assert (cs.double().cpu().sum(0) - ref_dy.sum((0, 1))).abs().max().item() < 1e-3

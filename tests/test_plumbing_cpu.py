@@ -24,7 +24,8 @@ from tests.helpers import product_config, make_batch, C0
 _QUERIES = {"maeclip_abi_version", "maeclip_last_error", "maeclip_device_count", "maeclip_gemm_colsum_rows",
             "maeclip_gemm_workspace", "maeclip_gemm_splitk", "maeclip_wgrad_grouped_workspace",
             "maeclip_ln_bwd_partial_rows", "maeclip_rows_colsum_partial_rows", "maeclip_mt_chunk",
-            "maeclip_clip_loss_workspace", "maeclip_wallclock_khz"}
+            "maeclip_clip_loss_workspace", "maeclip_wallclock_khz", "maeclip_unshuffle_bwd_partial_rows",
+            "maeclip_mae_loss_bwd_partial_rows"}
 
 
 class _StubLib:
