@@ -29,10 +29,16 @@
 #include "common.h"
 #include "../../include/maeclip.h"
 #include <type_traits>
+#include <stdlib.h>
 
 namespace {
 
 constexpr int MAXW = 8;          // max waves per workgroup (sized per launch to the tile count)
+
+bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && *v && *v != '0';
+}
 #define NW ((int)(blockDim.x >> 6))
 #define NTH ((int)blockDim.x)
 constexpr float LOG2E = 1.4426950408889634f;
@@ -363,7 +369,31 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
 }
 
 // ============================================================== backward
-template <typename T, int HD>
+// dS image (bf16 [npad keys][npad queries], phase 1 -> phase 2): 8-byte unit u
+// of row r lives at unit u ^ 4((r >> 2) & 1), so the eight rows a 32-lane half
+// of a ds_read_b64_tr_b16 touches fall on disjoint banks at npad = 224.
+__device__ __forceinline__ int dsimg_off(int row, int unit, int npad) {
+  return row * npad * 2 + ((unit ^ (((row >> 2) & 1) << 2)) << 3);
+}
+// B operand "dS^T" of the dQ product for keys kc..kc+31, queries q0 + (lane&15),
+// in the permuted k order of pack_p (element j <-> key kc + 16(j>>2) + 4g + (j&3))
+__device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane, int npad) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  v8s r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = kc + 16 * h + 4 * g + q;
+    v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, dsi + dsimg_off(row, (q0 >> 2) + p, npad)));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * h + e] = t[e];
+  }
+  return r;
+}
+
+// SDS (bf16 only, when the n x n image fits beside Q, K, V, dO): phase 1
+// keeps dS in LDS and phase 2 reads it back instead of recomputing S, dP and
+// the exponentials (the exp/VALU work bounds the hd = 32 decoder layers).
+template <typename T, int HD, bool SDS>
 __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
@@ -384,6 +414,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   float* L2 = (float*)(smem + (TWO ? 2 : 4) * img);
   float* Dv = L2 + npad;
   float* cs = Dv + npad;  // [NW][3*HD] bias-grad partials
+  char* dsi = (char*)(cs + NW * 3 * HD);   // SDS: [npad][npad] bf16
 
   const int HH = H * HD;
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
@@ -442,6 +473,14 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
           P[u][i] = p;
           dS[u][i] = p * dp[i];
         }
+        if (SDS) {
+          // row key, queries q0 + 4g .. +3; padding keys stored as zeros (their
+          // exp2(-lse) may overflow and would meet K's zero rows as 0 * inf)
+          v2u pk;
+          pk[0] = kok ? pack2bf(dS[u][0], dS[u][1]) : 0u;
+          pk[1] = kok ? pack2bf(dS[u][2], dS[u][3]) : 0u;
+          *(v2u*)(dsi + dsimg_off(key, (q0 >> 2) + g, npad)) = pk;
+        }
       }
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) {
@@ -486,10 +525,22 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
     __syncthreads();
   }
   // ---------------- phase 2: dQ (wave owns 16-query tiles)
+  if (SDS) __syncthreads();   // every wave's dS columns are in LDS
   for (int qt = wave; qt < nkt; qt += NW) {
     const int q0 = qt * 16;
     const int q = q0 + (lane & 15);
     const bool qok = q < n;
+    v4f dq[HD / 16];
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0, 0, 0, 0};
+    if constexpr (SDS) {
+      for (int kc = 0; kc < npad; kc += 32) {
+        const v8s bds = ds_frag(dsi, kc, q0, lane, npad);
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt)
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<HD>(Ki, kc, 16 * dt, lane), bds, dq[dt], 0, 0, 0);
+      }
+    } else {
     RowFrag<T, HD> qf[HD / 32], df[HD / 32];
 #pragma unroll
     for (int ks = 0; ks < HD / 32; ++ks) {
@@ -502,9 +553,6 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
       }
     }
     const float lq = L2[q], dq_ = Dv[q];
-    v4f dq[HD / 16];
-#pragma unroll
-    for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0, 0, 0, 0};
     for (int kc = 0; kc < npad; kc += 32) {
       v4f dST[2];
 #pragma unroll
@@ -530,6 +578,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
       }
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mma_rowsum<T, HD>(Ki, kc, 16 * dt, dST[0], dST[1], dq[dt], lane);
+    }
     }
     if (qok) {
       T* rowp = dqkv + (int64_t)q * a.ld_dqkv + h * HD;
@@ -571,18 +620,33 @@ template <typename T, int HD> size_t bwd_lds(int n, int nw) {
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
+template <typename T, int HD, bool SDS>
+void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS>), grid, dim3(nthreads), lds, s, a);
+}
+
 template <typename T, int HD>
 int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   // one wave per 16-row tile (no idle waves), at most MAXW
   const int tiles = (a.n + 15) / 16;
   const int nw = tiles < MAXW ? tiles : MAXW;
   const int nthreads = 64 * nw;
-  const size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
+  size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   dim3 grid((unsigned)(a.B * a.H));
   if (bwd) {
-    if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((attn_bwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);
+    // bf16: keep dS in LDS between the two phases when the n x n image fits
+    const size_t npad = (size_t)((a.n + 31) & ~31);
+    const size_t lds_sds = lds + npad * npad * 2;
+    bool sds = false;
+    if constexpr (std::is_same<T, bf16_t>::value) {
+      sds = lds_sds <= 163840 && !getenv_flag("MAECLIP_ATTN_NO_SDS");
+      if (sds) launch_bwd<T, HD, true>(a, grid, nthreads, lds_sds, s);
+    }
+    if (!sds) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);

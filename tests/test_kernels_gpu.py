@@ -95,10 +95,11 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
+@pytest.mark.parametrize("sds", [True, False])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
-                                   (1, 197, 2, 32), (1, 256, 2, 64)])
-def test_attention_fwd_bwd(dev, dtype, shape):
+                                   (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32)])
+def test_attention_fwd_bwd(dev, dtype, shape, sds, monkeypatch):
     """fp32 parity mode holds two [n][hd] f32 images at a time in the
     backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well."""
     B, n, H, hd = shape
@@ -462,7 +463,8 @@ def test_mae_loss_kernels_vs_torch(dev, dtype, cfg):
     tolg = 1e-5 if dtype == torch.float32 else 1e-2
     assert (d[:, 1:, :P] - pr.grad).abs().max().item() < tolg * gs
     assert torch.count_nonzero(d[:, 0]) == 0 and torch.count_nonzero(d[:, :, P:]) == 0
-    assert (cs.double().cpu().sum(0) - d[:, :, :P].sum((0, 1))).abs().max().item() < 1e-4 * gs * L_
+    # bias-gradient partials are summed from the fp32 values (before dpred's rounding)
+    assert (cs.double().cpu().sum(0) - pr.grad.sum((0, 1))).abs().max().item() < tolg * gs * L_
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -474,7 +476,7 @@ def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
     ids_s, ids_r, mask, _ = K.mask_ids(B, L_, keep, seed=2, step=1, sample_offset=0, device=dev)
     dx = _rand((B, keep + 1, D), torch.float32, dev, seed=61)
     dy, dpos, dcls = K.tokens_bwd(dx, ids_r, B, L_, keep, dtype)
-    assert torch.equal(dy.float().view(B, keep, D), dx[:, 1:].to(dtype).float())
+    assert torch.equal(dy.float().view(B, keep, D).cpu(), dx[:, 1:].to(dtype).float().cpu())
     ref = torch.zeros(L_ + 1, D, dtype=torch.float64)
     x64 = dx.double().cpu()
     ref[0] = x64[:, 0].sum(0)
@@ -494,6 +496,6 @@ def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
         kept = r[b] < keep
         ref_dy[b, 1 + r[b][kept]] = o64[b, 1:][kept]
         ref_dm += o64[b, 1:][~kept].sum(0)
-    assert torch.equal(dy2.float().view(B, keep + 1, Dd), ref_dy.float().to(dtype).float().to(dev).cpu())
+    assert torch.equal(dy2.float().view(B, keep + 1, Dd).cpu(), ref_dy.float().to(dtype).float())
     assert (dmask.double().cpu().sum(0) - ref_dm).abs().max().item() < 1e-3
     assert (cs.double().cpu().sum(0) - ref_dy.sum((0, 1))).abs().max().item() < 1e-3
