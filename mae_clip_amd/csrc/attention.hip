@@ -423,13 +423,20 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   bwd_prologue<T, HD, !TWO>(Qi, Ki, Vi, Di, L2, Dv, qkv + h * HD, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv,
                             O, dO, a.ld_o, a.lse + ((int64_t)b * H + h) * n, 1.f / (a.scale * LOG2E), n, npad);
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) cs[i] = 0.f;
+  const int nkt = (n + 15) >> 4;
+  if (SDS) {
+    // phase 1 writes dS rows for keys < 16 nkt; phase 2 reads keys < npad:
+    // the (at most 16) rows in between are zero
+    v4u* tail = (v4u*)(dsi + (size_t)nkt * 16 * npad * 2);
+    const int nv = (npad - nkt * 16) * npad * 2 / 16;
+    for (int i = threadIdx.x; i < nv; i += NTH) tail[i] = v4u{0u, 0u, 0u, 0u};
+  }
   __syncthreads();
 
   const float c = a.scale * LOG2E;
   T* dqkv = (T*)a.dqkv + (int64_t)b * n * a.ld_dqkv;
 
   // ---------------- phase 1: dK, dV (wave owns 16-key tiles)
-  const int nkt = (n + 15) >> 4;
   for (int kt = wave; kt < nkt; kt += NW) {
     const int k0 = kt * 16;
     const int key = k0 + (lane & 15);
@@ -638,12 +645,15 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   dim3 grid((unsigned)(a.B * a.H));
   if (bwd) {
-    // bf16: keep dS in LDS between the two phases when the n x n image fits
+    // bf16, opt-in (MAECLIP_ATTN_SDS=1): keep dS in LDS between the two phases
+    // when the n x n image fits. Measured slower on MI355X at the path's shapes
+    // (decoder n = 197, hd = 32: 355 vs 224 us; the 100 KB image halves the
+    // workgroups per CU), so the default recomputes S / dP for dQ.
     const size_t npad = (size_t)((a.n + 31) & ~31);
     const size_t lds_sds = lds + npad * npad * 2;
     bool sds = false;
     if constexpr (std::is_same<T, bf16_t>::value) {
-      sds = lds_sds <= 163840 && !getenv_flag("MAECLIP_ATTN_NO_SDS");
+      sds = lds_sds <= 163840 && getenv_flag("MAECLIP_ATTN_SDS");
       if (sds) launch_bwd<T, HD, true>(a, grid, nthreads, lds_sds, s);
     }
     if (!sds) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);

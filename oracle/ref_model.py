@@ -301,10 +301,11 @@ class DistilBertEmbeddings(nn.Module):
         self.word_embeddings = nn.Embedding(vocab, dim)
         self.position_embeddings = nn.Embedding(max_pos, dim)
         self.LayerNorm = nn.LayerNorm(dim, eps=1e-12)
+        self.dropout = nn.Dropout(0.1)   # HF DistilBertConfig dropout (identity in eval mode)
 
     def forward(self, ids):
         pos = torch.arange(ids.shape[1])
-        return self.LayerNorm(self.word_embeddings(ids) + self.position_embeddings(pos)[None])
+        return self.dropout(self.LayerNorm(self.word_embeddings(ids) + self.position_embeddings(pos)[None]))
 
 
 class DistilBertAttention(nn.Module):
@@ -315,6 +316,7 @@ class DistilBertAttention(nn.Module):
         self.k_lin = nn.Linear(dim, dim)
         self.v_lin = nn.Linear(dim, dim)
         self.out_lin = nn.Linear(dim, dim)
+        self.dropout = nn.Dropout(0.1)   # attention_dropout (identity in eval mode)
 
     def forward(self, x, mask):
         B, T, D = x.shape
@@ -323,7 +325,7 @@ class DistilBertAttention(nn.Module):
         q, k, v = sh(self.q_lin(x)), sh(self.k_lin(x)), sh(self.v_lin(x))
         s = (q @ k.transpose(-1, -2)) * hd ** -0.5
         s = s.masked_fill(mask.view(B, 1, 1, T) == 0, torch.finfo(s.dtype).min)
-        o = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, T, D)
+        o = (self.dropout(s.softmax(-1)) @ v).transpose(1, 2).reshape(B, T, D)
         return self.out_lin(o)
 
 
@@ -332,9 +334,10 @@ class DistilBertFFN(nn.Module):
         super().__init__()
         self.lin1 = nn.Linear(dim, hidden)
         self.lin2 = nn.Linear(hidden, dim)
+        self.dropout = nn.Dropout(0.1)   # HF dropout (identity in eval mode)
 
     def forward(self, x):
-        return self.lin2(F.gelu(self.lin1(x)))
+        return self.dropout(self.lin2(F.gelu(self.lin1(x))))
 
 
 class DistilBertLayer(nn.Module):

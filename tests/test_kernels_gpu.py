@@ -103,6 +103,9 @@ def test_attention_fwd_bwd(dev, dtype, shape, sds, monkeypatch):
     """fp32 parity mode holds two [n][hd] f32 images at a time in the
     backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well."""
     B, n, H, hd = shape
+    if sds:
+        # bf16 backward keeps dS in LDS for dQ instead of recomputing S/dP (opt-in)
+        monkeypatch.setenv("MAECLIP_ATTN_SDS", "1")
     scale = hd ** -0.5
     qkv = _rand((B * n, 3 * H * hd), dtype, dev, seed=11)
     o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 for ctr in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS" "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS" "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   tag=$(echo $ctr | cut -d' ' -f1)
-  timeout -k 10 120 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/$tag -o run -- python tools/gemm_one.py "$@" > /dev/null 2>&1 || echo "fail $ctr"
+  timeout -s KILL 90 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/$tag -o run -- python tools/gemm_one.py "$@" > /dev/null 2>&1 || echo "fail $ctr"
 done
 python - <<'PY'
 import csv, glob, collections
