@@ -20,12 +20,21 @@ def read():
 
 
 cases = [("dec fc2 dgrad none", D, 2048, 512, K.EPI_NONE), ("dec fc2 dgrad mulaux", D, 2048, 512, K.EPI_MUL_AUX),
-         ("enc fc1 fwd none", E, 3072, 768, None)]
+         ("dec fc1 fwd gelu_d", D, 2048, 512, ("fwd", K.EPI_GELU_D)), ("dec fc2 fwd resid", D, 512, 2048, ("fwd", K.EPI_RESID)),
+         ("enc fc1 fwd none", E, 3072, 768, ("fwd", K.EPI_NONE))]
 for name, M, N, Kd, epi in cases:
-    if epi is None:
+    if isinstance(epi, tuple):
         x = (torch.randn(M, Kd, device=dev) * 0.5).to(torch.bfloat16)
         w = (torch.randn(N, Kd, device=dev) * 0.5).to(torch.bfloat16)
-        f = lambda: K.linear_fwd(x, w)
+        e = epi[1]
+        if e == K.EPI_GELU_D:
+            bias, aux_out = torch.randn(N, device=dev), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            f = lambda: K.linear_fwd(x, w, bias, epilogue=e, aux_out=aux_out)
+        elif e == K.EPI_RESID:
+            bias, res = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+            f = lambda: K.linear_fwd(x, w, bias, out_dtype=torch.float32, epilogue=e, resid=res)
+        else:
+            f = lambda: K.linear_fwd(x, w)
     else:
         dy = (torch.randn(M, Kd, device=dev) * 0.5).to(torch.bfloat16)
         w = (torch.randn(Kd, N, device=dev) * 0.5).to(torch.bfloat16)
