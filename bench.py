@@ -285,23 +285,18 @@ def main():
     if not args.no_kernel_timer:
         K.LAUNCH_HOOK = timer.hook
 
-    # one HIP graph per step (mae_clip_amd.graph): step 1 eager, step 2 captured,
-    # then replays. Data-parallel runs and --gemm-table stay eager.
-    use_graph = not use_dp and not args.no_graph and not args.gemm_table
-    runner = CapturedStep(model, opt, enabled=use_graph, eager_steps=2)
+    # one HIP graph per step (mae_clip_amd.graph): steps 1-2 eager, step 3
+    # captured, then replays -- at N=1 and, with the RCCL collectives captured
+    # inside the graph, at N>1. --gemm-table stays eager.
+    use_graph = not args.no_graph and not args.gemm_table
+    runner = CapturedStep(model, opt, enabled=use_graph, eager_steps=2, dp=dp)
+    use_graph = runner.enabled
     warmup = max(args.warmup, 3) if use_graph else max(args.warmup, 2)
 
     def step():
-        if dp is None:
-            # after capture the graph's static input buffers ARE the batch
-            # (synthetic inputs resident in HBM): no per-step copy
-            return runner.step(runner.static if runner.static is not None else batch)
-        opt.zero_grad(set_to_none=True)
-        loss = model(batch)
-        loss.backward()
-        dp.sync_gradients()
-        opt.step()
-        return loss
+        # after capture the graph's static input buffers ARE the batch
+        # (synthetic inputs resident in HBM): no per-step copy
+        return runner.step(runner.static if runner.static is not None else batch)
 
     # warm-up: time every GEMM launch of the second (eager, warm) step to find
     # the dominant shape; afterwards only that shape's launches are bracketed

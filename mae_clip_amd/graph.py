@@ -19,6 +19,14 @@ Usage (drop-in around the reference's train_epoch body):
     runner = CapturedStep(model, optimizer)
     for batch in loader:
         loss = runner.step(batch)      # model(batch); loss.backward(); optimizer.step()
+
+Data parallel (CapturedStep(..., dp=DataParallel(model))): the step becomes
+model(batch); backward; dp.sync_gradients(); optimizer.step(), and the RCCL
+collectives (the embedding all-gather of the forward, the bucketed gradient
+all-reduces launched from the backward's hooks) are captured with it: every
+rank replays the same collective sequence, so the N>1 step is one graph launch
+per rank as at N=1. The gloo backend (host-staged copies) cannot be captured:
+CapturedStep then stays eager.
 """
 from __future__ import annotations
 
@@ -26,9 +34,12 @@ import torch
 
 
 class CapturedStep:
-    def __init__(self, model, optimizer, enabled: bool = True, eager_steps: int = 1):
+    def __init__(self, model, optimizer, enabled: bool = True, eager_steps: int = 1, dp=None):
         self.model = model
         self.opt = optimizer
+        self.dp = dp
+        if dp is not None and torch.distributed.get_backend(dp.group) != "nccl":
+            enabled = False
         self.enabled = enabled
         self.eager_steps = max(1, eager_steps)
         self.graph = None
@@ -47,6 +58,8 @@ class CapturedStep:
         self.opt.zero_grad(set_to_none=True)
         loss = self.model(batch)
         loss.backward()
+        if self.dp is not None:
+            self.dp.sync_gradients()
         self.opt.step()
         # detached: a caller holding the loss must not keep this step's autograd
         # graph (and its AccumulateGrad nodes, bound to the eager stream) alive
@@ -64,6 +77,8 @@ class CapturedStep:
         with torch.cuda.graph(g, capture_error_mode="relaxed"):
             loss = self.model(self.static)
             loss.backward()
+            if self.dp is not None:
+                self.dp.sync_gradients()
             self.opt.step()
         # capture recorded the work without running it: undo its host-side counting
         self.model.step = model_step

@@ -93,3 +93,46 @@ def test_product_data_parallel_equals_full_batch(dev):
         for o in res:
             assert (o["grads"][n] - g).abs().max().item() / sc < 1e-4, n
         assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
+
+
+def _captured_dp_rank(rank, world, port, out):
+    """One RCCL rank (the box has one GPU): CapturedStep with DataParallel --
+    the embedding all-gather and the bucketed gradient all-reduces are captured
+    in the step's HIP graph -- against the same DP steps run eagerly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from mae_clip_amd import _lib
+        from mae_clip_amd.distributed import DataParallel
+        from mae_clip_amd.optim import AdamW
+        from mae_clip_amd.graph import CapturedStep
+        from tests.helpers import make_batch
+        _lib.load()
+        res = {}
+        for captured in (False, True):
+            m = _model("bf16").train()
+            dp = DataParallel(m, bucket_mb=4.0)
+            opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+            runner = CapturedStep(m, opt, enabled=captured, eager_steps=2, dp=dp)
+            losses = []
+            for it in range(5):
+                b = {k: v.cuda() for k, v in make_batch(8, 32, seed=it).items()}
+                losses.append(runner.step(b).item())
+            torch.cuda.synchronize()
+            res[captured] = dict(losses=losses, enabled=runner.enabled, captures=runner.captures,
+                                 params={n: p.detach().cpu() for n, p in m.named_parameters()})
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_captured_step_with_rccl_data_parallel(dev):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_captured_dp_rank, args=(1, _free_port(), out), nprocs=1, join=True)
+    eager, graph = out[0][False], out[0][True]
+    assert graph["enabled"] and graph["captures"] == 1
+    assert eager["losses"] == graph["losses"], (eager["losses"], graph["losses"])
+    for n, p in eager["params"].items():
+        assert torch.equal(p, graph["params"][n]), n
