@@ -31,9 +31,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0    # MI355X dense fp8 (block-scaled e4m3) MFMA
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md; 6.3 TB/s measured copy)
 PEAK_F32_TFLOPS = 157.3
 IMG_FLOPS_C2 = 60.2e9       # algorithmic FLOP / image, SURVEY.md §8d / Appendix C
+
+# BASELINE.json configs by SURVEY.md §8 label. The driver's default line is C2
+# (N=1) / C3 (N>1: the same 256 images per GPU, global batch 256*N).
+CONFIGS = {
+    "c2": dict(model=dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, mask_ratio=0.75),
+               batch=256, flops=60.2e9,
+               workload="C2/C3: ViT-B/16 224 MAE(0.75)+CLIP, 8x512 decoder, DistilBERT-6 frozen T=25, AdamW, "
+                        "bf16 MFMA / fp32 master"),
+    "c1": dict(model=dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, mask_ratio=0.0),
+               batch=256, flops=107.3e9,
+               workload="C1: ViT-B/16 224 CLIP-only (mask 0, the reference's path), DistilBERT-6 frozen T=25, "
+                        "AdamW, bf16 MFMA / fp32 master"),
+    "c4": dict(model=dict(model_name="vit_large_patch14_336", size=336, image_embedding=1024, mask_ratio=0.75),
+               batch=128, flops=376.4e9,
+               workload="C4: ViT-L/14 336 MAE(0.75)+CLIP, 8x512 decoder, DistilBERT-6 frozen T=25, AdamW, "
+                        "fp32 master"),
+}
 
 
 def synthetic_batch(B, S, T, seed, device):
@@ -233,8 +251,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--mask-ratio", type=float, default=0.75)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE.json config (SURVEY.md §8 labels); the default line is C2/C3")
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
+    ap.add_argument("--mask-ratio", type=float, default=None)
+    ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
+                    help="GEMM operand precision (fp8: OCP e4m3 forward/dgrad GEMMs, per-tensor delayed scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
@@ -272,14 +294,22 @@ def main():
     from mae_clip_amd.distributed import DataParallel
     from mae_clip_amd.graph import CapturedStep
 
-    model = build_model(dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6,
-                             mask_ratio=args.mask_ratio, decoder_embed_dim=512, decoder_depth=8,
-                             decoder_num_heads=16, precision="bf16",
+    cfg = CONFIGS[args.config]
+    if args.batch is None:
+        args.batch = cfg["batch"]
+    mcfg = dict(cfg["model"])
+    if args.mask_ratio is not None:
+        mcfg["mask_ratio"] = args.mask_ratio
+    args.mask_ratio = mcfg["mask_ratio"]
+    img_flops = cfg["flops"] if args.mask_ratio == cfg["model"]["mask_ratio"] else None
+    size = mcfg["size"]
+    model = build_model(dict(mcfg, text_layers=6, decoder_embed_dim=512, decoder_depth=8,
+                             decoder_num_heads=16, precision=args.precision,
                              side_stream=not args.no_side_stream)).to(device)
     model.train()
     dp = DataParallel(model) if use_dp else None
     opt = AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
-    batch = synthetic_batch(args.batch, 224, 25, 1000 + rank, device)
+    batch = synthetic_batch(args.batch, size, 25, 1000 + rank, device)
 
     timer = KernelTimer()
     if not args.no_kernel_timer:
@@ -343,30 +373,36 @@ def main():
             tf = flops / avg_s / 1e12
             gbs = nbytes / avg_s / 1e9
             # which roof bounds it: arithmetic intensity vs the ridge point
+            # (dense MFMA peak of the kernel's operand type: bf16 2.5, fp8 5.0 PF/s)
+            mpeak = PEAK_FP8_TFLOPS if " fp8" in key else PEAK_BF16_TFLOPS
             ai = flops / nbytes
-            ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+            ridge = mpeak * 1e12 / (PEAK_HBM_GBS * 1e9)
             traffic, tsrc = pmc_traffic(key)
             if ai >= ridge:
-                bound, ach, peak, unit = "mfma", tf, PEAK_BF16_TFLOPS, "TFLOP/s"
+                bound, ach, peak, unit = "mfma", tf, mpeak, "TFLOP/s"
             else:
                 bound, ach, peak, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
             roof = {"bound": bound, "kernel": "gemm " + key, "achieved": round(ach, 1), "peak": peak, "unit": unit,
                     "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                     "traffic_source": tsrc, "algorithmic_bytes": nbytes, "flops": flops,
                     "arith_intensity": round(ai, 1), "ridge": round(ridge, 1),
-                    "tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_BF16_TFLOPS, 4), "gbs": round(gbs, 1),
+                    "tflops": round(tf, 1), "mfma_frac": round(tf / mpeak, 4), "gbs": round(gbs, 1),
                     "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
                     "avg_launch_us": round(avg_s * 1e6, 1), "launches": nl,
-                    "step_tflops": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12, 1),
-                    "step_frac": round(IMG_FLOPS_C2 * args.batch / (ms / 1000.0) / 1e12 / PEAK_BF16_TFLOPS, 4)}
-        out = {"metric": "images/sec/node ViT-B/16 CLIP+MAE step", "value": round(value, 2), "unit": "images/s",
+                    "step_tflops": round(img_flops * args.batch / (ms / 1000.0) / 1e12, 1) if img_flops else None,
+                    "step_frac": round(img_flops * args.batch / (ms / 1000.0) / 1e12 / PEAK_BF16_TFLOPS, 4)
+                    if img_flops else None, "step_frac_peak": "bf16 dense 2.5 PF/s"}
+        metric = ("images/sec/node ViT-B/16 CLIP+MAE step" if args.config != "c4"
+                  else "images/sec/node ViT-L/14@336 CLIP+MAE step")
+        out = {"metric": metric, "value": round(value, 2), "unit": "images/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
                "data": "synthetic (uint8 pixels ImageNet-normalised, input_ids randint(5,300)), random-init weights",
-               "config": {"workload": "C2/C3: ViT-B/16 224 MAE(0.75)+CLIP, 8x512 decoder, DistilBERT-6 frozen "
-                                      "T=25, AdamW, bf16 MFMA / fp32 master",
-                          "global_batch": global_batch, "per_gpu_batch": args.batch, "image_size": 224,
-                          "mask_ratio": args.mask_ratio, "parallelism": f"dp{world}"},
+               "config": {"workload": cfg["workload"].replace("fp32 master", f"{args.precision} MFMA / fp32 master")
+                          if args.config == "c4" else cfg["workload"], "label": args.config.upper(),
+                          "global_batch": global_batch, "per_gpu_batch": args.batch, "image_size": size,
+                          "mask_ratio": args.mask_ratio, "parallelism": f"dp{world}",
+                          "img_flops": img_flops},
                "loss": round(loss.item(), 4), "roofline": roof,
                "step_mode": "hip-graph" if use_graph else "eager",
                "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size()} if use_dp else None}

@@ -30,6 +30,8 @@ extern "C" {
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
 #endif
+#define MAECLIP_FP8_E4M3 2   /* OCP float8 e4m3fn (gfx950), max 448 */
+#define MAECLIP_FP8_E5M2 3   /* OCP float8 e5m2, max 57344 */
 
 int32_t maeclip_abi_version(void);
 const char* maeclip_last_error(void);
@@ -82,6 +84,24 @@ typedef struct {
   float* workspace;
 } maeclip_gemm_args;
 int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
+/* fp8 GEMM (C4 path; replaces the nn.Linear matmuls of the timm / ViTMAE
+ * blocks, modules.py:17-19, when precision = "fp8"). A [M, lda] and B [N, ldb]
+ * are OCP fp8 bytes, both KC (K contiguous, K % 128 == 0, lda, ldb % 16 == 0);
+ * args->dtype is A's format (MAECLIP_FP8_E4M3 / _E5M2), B is e4m3. The
+ * block-scaled 16x16x128 MFMA accumulates in fp32 and the epilogue applies
+ * scale_a[m] * scale_b[n] * alpha before bias / epilogue (args->epilogue as
+ * maeclip_gemm; no split-K, beta must be 0). M, N >= 256, N % 8 == 0. */
+int32_t maeclip_gemm_fp8(const maeclip_gemm_args* args, const float* scale_a, const float* scale_b, void* stream);
+/* Row-wise fp8 quantisation: q[r, :] = rne(x[r, :] / s[r]), s[r] = amax(x[r, :]) /
+ * FMT_MAX (1 when the row is zero). x bf16 or f32 [rows, ld]; q [rows, ldq]
+ * bytes; fmt MAECLIP_FP8_E4M3 (activations, weights) or _E5M2 (gradients). */
+int32_t maeclip_quant_rows_fp8(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ld, void* q,
+                               int64_t ldq, float* scales, int32_t fmt, void* stream);
+/* W^T quantisation (e4m3) from the fp32 master W [rows, ld]: qt [cols, ldq]
+ * (ldq % 16 == 0), one scale per column of W (per row of W^T). */
+int64_t maeclip_quant_cols_fp8_workspace(int64_t rows, int64_t cols);
+int32_t maeclip_quant_cols_fp8(const float* w, int64_t rows, int64_t cols, int64_t ld, void* qt, int64_t ldq,
+                               float* scales, float* workspace, int64_t ws_bytes, void* stream);
 int64_t maeclip_gemm_colsum_rows(int64_t M);
 /* scratch bytes maeclip_gemm may use for *args when args->splitk <= 1 (pass
  * them as args->workspace; a NULL workspace is always valid, just slower) */

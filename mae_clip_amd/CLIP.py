@@ -67,7 +67,7 @@ class CLIPModel(nn.Module):
     # ------------------------------------------------------------------
     def _weight_cache(self):
         if self._cache is None:
-            c = WeightCache()
+            c = WeightCache(fp8=self.precision == "fp8")
             self.image_encoder.model.register_weights(c)
             if self.mae_decoder is not None:
                 self.mae_decoder.register_weights(c)
@@ -141,8 +141,10 @@ class CLIPModel(nn.Module):
             dspec = Fn.DecSpec(B=B, L=L, keep=keep, dtype=dtype, w_T=cache.get(dec.decoder_embed.weight, dtype))
             xd = Fn.DecoderEmbedFn.apply(latent, ids_shuffle, ids_restore, dspec, dec.decoder_embed.weight,
                                          dec.decoder_embed.bias, dec.mask_token, dec.decoder_pos_embed)
+            # fp8 mode keeps the decoder on bf16: its K = 512 GEMMs are bound by
+            # their epilogue traffic, so fp8 operands would only add quantisation passes
             xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache,
-                           chunk=(CFG.dp_decoder_chunk or None) if world > 1 else None)
+                           chunk=(CFG.dp_decoder_chunk or None) if world > 1 else None, fp8=False)
             wp_T, bp_pad = cache.get(dec.decoder_pred.weight, dtype), None
             P = wp_T.shape[0]
             if dtype == torch.bfloat16 and P % 64:

@@ -126,6 +126,10 @@ _SIGS = {
     "maeclip_gemm_colsum_rows": (c_i64, [c_i64]),
     "maeclip_gemm_workspace": (c_i64, [C.POINTER(GemmArgs)]),
     "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
+    "maeclip_gemm_fp8": (c_i32, [C.POINTER(GemmArgs), c_vp, c_vp, c_vp]),
+    "maeclip_quant_rows_fp8": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "maeclip_quant_cols_fp8_workspace": (c_i64, [c_i64, c_i64]),
+    "maeclip_quant_cols_fp8": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "maeclip_wgrad_grouped_workspace": (c_i64, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32]),
     "maeclip_wgrad_grouped": (c_i32, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32, c_f32, c_vp, c_i64, c_vp]),
     "maeclip_image_normalize_u8": (c_i32, [C.POINTER(ImageU8Args), c_vp]),

@@ -63,7 +63,7 @@ text_dropout = 0.1
 text_attention_dropout = 0.1
 
 # ---- numerics / determinism
-precision = "bf16"         # "bf16" (perf) or "fp32" (parity mode, exact-f32 MFMA)
+precision = "bf16"         # "bf16" (perf), "fp8" (C4: e4m3/e5m2 stack GEMMs, bf16 elsewhere) or "fp32" (parity mode)
 mask_seed = 2
 dropout_seed = 1234
 # ---- scheduling

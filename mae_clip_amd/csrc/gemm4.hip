@@ -59,20 +59,20 @@ __device__ __forceinline__ int bmap(int l, int sub) { return (l & 31) + ((l >> 5
 // results are never stored.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-__device__ __forceinline__ rsrc_t make_rsrc(const bf16_t* base, int64_t bytes) {
+__device__ __forceinline__ rsrc_t make_rsrc(const char* base, int64_t bytes) {
   const int nrec = (int)(bytes < 0x7fffffff ? (bytes > 0 ? bytes : 0) : 0x7fffffff);
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
 }
 
 // per-lane byte offset of wave-instruction i (0, 1) of half `sub` (0, 1) of an operand
-template <int LAY, bool ISA>
+template <int LAY, bool ISA, int ESZ = 2>
 __device__ __forceinline__ int half_voffset(int64_t ld, int sub, int i, int wave, int lane) {
   const int q = i * 8 + wave;
   if (LAY == LAY_KC) {
     const int r = q * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int g = ISA ? amap(r, sub) : bmap(r, sub);
-    return (int)(g * ld * 2) + c * 16;
+    return (int)(g * ld * ESZ) + c * 16;
   } else {
     const int kr = q * 4 + (lane >> 4);
     const int c = (lane & 15) ^ (swz_rc(kr) >> 1);
@@ -119,6 +119,41 @@ __device__ __forceinline__ v8s frag(const char* lds, int rs, int ks, int lane) {
     __builtin_amdgcn_sched_barrier(0);       \
     asm volatile("" ::: "memory");           \
   } while (0)
+
+// The 16 MFMAs of one quadrant: rows i0.. of acc (4 A fragments), columns j0..
+// (2 B fragments). Each operand fragment is two 16-B LDS chunks of a row (k
+// chunks g and 4 + g of the 128-byte K-tile row). bf16: two 16x16x32 MFMAs
+// (ks = 0, 1). fp8 (F8 = 1: A e4m3, F8 = 2: A e5m2; B e4m3): the same 32 bytes
+// are one 16x16x128 block-scaled MFMA operand (all block scales 2^0; the
+// per-row / per-column dequantisation scales are applied in the epilogue). A
+// and B fragments put identical k's at identical lane/byte positions, so the
+// hardware's k order inside the 128 need not be known.
+__device__ __forceinline__ v8i cat_frag(v8s a, v8s b) {
+  const v4i x = __builtin_bit_cast(v4i, a), y = __builtin_bit_cast(v4i, b);
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int F8>
+__device__ __forceinline__ void quad_mma(v4f (&acc)[8][4], int i0, int j0, const v8s (&fbq)[2][2],
+                                         const v8s (&fa)[4][2]) {
+  if constexpr (F8 == 0) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbq[j][ks], fa[i][ks], acc[i0 + i][j0 + j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const v8i a8 = cat_frag(fa[i][0], fa[i][1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            cat_frag(fbq[j][0], fbq[j][1]), a8, acc[i0 + i][j0 + j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+    }
+  }
+}
 
 // Epilogue. Fragment (i, j) of the wave covers rows m0 + 128 wm + 64 (i>>2) +
 // 16 (i&3) and columns n0 + 64 wn + 32 (j>>1) + 16 (j&1); the MFMA leaves lane
@@ -167,9 +202,12 @@ __device__ __forceinline__ void epilogue4_slab(float* __restrict__ slab, int M, 
   }
 }
 
-template <typename OutT, int EPI>
+// sa / sb (fp8 only): per-row dequantisation scale of A [M] and per-column
+// scale of B [N]; the product scales the accumulator before alpha / bias.
+template <typename OutT, int EPI, bool F8 = false>
 __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&acc)[8][4], int64_t z, int m0, int n0,
-                                          int wm, int wn, int lane) {
+                                          int wm, int wn, int lane, const float* __restrict__ sa = nullptr,
+                                          const float* __restrict__ sb = nullptr) {
   constexpr bool LOAD_AUX = EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   constexpr bool LOAD_RES = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   const int M = (int)args.M, N = (int)args.N;
@@ -220,8 +258,18 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       const int i = c, ni = q;
       const int m = rbase + 64 * (i >> 2) + 16 * (i & 3);
       const int n = cb0 + 32 * ni;
-      v4f lo = acc[i][2 * ni] * alpha + bias8[ni][0];
-      v4f hi = acc[i][2 * ni + 1] * alpha + bias8[ni][1];
+      v4f lo, hi;
+      if constexpr (F8) {
+        // dequantise: per-row A scale x per-column B scale (re-read per chunk
+        // from L1/L2: keeps the register budget of the aux epilogues)
+        const float sam = sa[min(m, M - 1)] * alpha;
+        const int nc = min(n, N - 8);
+        lo = acc[i][2 * ni] * (*(const v4f*)(sb + nc) * sam) + bias8[ni][0];
+        hi = acc[i][2 * ni + 1] * (*(const v4f*)(sb + nc + 4) * sam) + bias8[ni][1];
+      } else {
+        lo = acc[i][2 * ni] * alpha + bias8[ni][0];
+        hi = acc[i][2 * ni + 1] * alpha + bias8[ni][1];
+      }
       if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
         v4f dlo = lo, dhi = hi;   // GELU: aux_out <- pre-activation
         if (EPI == EPI_GELU_D) {
@@ -327,8 +375,8 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
 // One unit of work of the persistent loop: a 256x256 output tile of one
 // problem and its K range (a split-K slice or the whole K).
 struct Unit4 {
-  const bf16_t* A;
-  const bf16_t* B;
+  const char* A;
+  const char* B;
   int64_t lda, ldb;
   int M, N, K;        // problem sizes (K = full reduction length)
   int m0, n0;
@@ -357,8 +405,16 @@ struct WgGroup {
   WgProb p[WG_MAX];
 };
 
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP>
-__device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp) {
+// F8: 0 = bf16 operands (K-tile 64); 1 / 2 = fp8 operands, A e4m3 / e5m2 and
+// B e4m3 (K-tile 128 = the same 128 bytes per row), per-row A scales sa[M] and
+// per-column B scales sb[N] applied in the epilogue.
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0>
+__device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp,
+                                           const float* __restrict__ sa = nullptr,
+                                           const float* __restrict__ sb = nullptr) {
+  static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
+  constexpr int ESZ = F8 ? 1 : 2;      // operand bytes per element
+  constexpr int KT = 128 / ESZ;        // elements per K-tile (128 bytes per row)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -370,13 +426,13 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   int T, gn = 1, klen = 0;
   if (GRP) {
     T = gp->T * gp->S;
-    klen = ((gp->Mtok + gp->S - 1) / gp->S + 63) / 64 * 64;
+    klen = ((gp->Mtok + gp->S - 1) / gp->S + KT - 1) / KT * KT;
   } else {
     const int gm = ((int)args.M + 255) / 256;
     gn = ((int)args.N + 255) / 256;
     T = gm * gn;
     const int S = SPLIT ? args.splitk : 1;
-    klen = (((int)args.K + S - 1) / S + 63) / 64 * 64;
+    klen = (((int)args.K + S - 1) / S + KT - 1) / KT * KT;
   }
   auto unit = [&](int u) {
     Unit4 w;
@@ -386,8 +442,8 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       while (p + 1 < gp->np && gp->p[p + 1].tile_begin <= tile) ++p;
       const WgProb& q = gp->p[p];
       const int local = tile - q.tile_begin, gnp = (q.K + 255) / 256;
-      w.A = q.dy;
-      w.B = q.x;
+      w.A = (const char*)q.dy;
+      w.B = (const char*)q.x;
       w.lda = q.ldy;
       w.ldb = q.ldx;
       w.M = q.N;
@@ -398,8 +454,8 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       w.slice = sl;
       w.prob = p;
     } else {
-      w.A = (const bf16_t*)args.A + z * args.strideA;
-      w.B = (const bf16_t*)args.B + z * args.strideB;
+      w.A = (const char*)args.A + z * args.strideA * ESZ;
+      w.B = (const char*)args.B + z * args.strideB * ESZ;
       w.lda = args.lda;
       w.ldb = args.ldb;
       w.M = (int)args.M;
@@ -412,7 +468,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     }
     w.kbeg = w.slice * klen;
     const int kend = min(w.K, w.kbeg + klen);
-    w.nt = kend > w.kbeg ? (kend - w.kbeg) / 64 : 0;
+    w.nt = kend > w.kbeg ? (kend - w.kbeg) / KT : 0;
     return w;
   };
 
@@ -432,23 +488,23 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        vA[sub][i] = half_voffset<LA, true>(w.lda, sub, i, wave, lane);
-        vB[sub][i] = half_voffset<LB, false>(w.ldb, sub, i, wave, lane);
+        vA[sub][i] = half_voffset<LA, true, ESZ>(w.lda, sub, i, wave, lane);
+        vB[sub][i] = half_voffset<LB, false, ESZ>(w.ldb, sub, i, wave, lane);
       }
   };
   // half h of K-tile t of unit w: 0 = Am0, 1 = Am1, 2 = Bn0, 3 = Bn1. The
   // K-tile advance is along the row (KC) or down the k-rows (RC).
   auto issue = [&](const Unit4& w, const int (&vA)[2][2], const int (&vB)[2][2], int t, int h) {
     char* dst = smem + (t & 1) * BUF + h * HALF;
-    const int k0 = w.kbeg + t * 64;
+    const int k0 = w.kbeg + t * KT;
     if (h < 2) {
-      const rsrc_t rs = LA == LAY_KC ? make_rsrc(w.A + (int64_t)w.m0 * w.lda, ((int64_t)w.M - w.m0) * w.lda * 2)
-                                     : make_rsrc(w.A + w.m0, ((int64_t)w.K * w.lda - w.m0) * 2);
-      issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? 2 : (int)(w.lda * 2)), dst, wave);
+      const rsrc_t rs = LA == LAY_KC ? make_rsrc(w.A + (int64_t)w.m0 * w.lda * ESZ, ((int64_t)w.M - w.m0) * w.lda * ESZ)
+                                     : make_rsrc(w.A + (int64_t)w.m0 * ESZ, ((int64_t)w.K * w.lda - w.m0) * ESZ);
+      issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? ESZ : (int)(w.lda * ESZ)), dst, wave);
     } else {
-      const rsrc_t rs = LB == LAY_KC ? make_rsrc(w.B + (int64_t)w.n0 * w.ldb, ((int64_t)w.N - w.n0) * w.ldb * 2)
-                                     : make_rsrc(w.B + w.n0, ((int64_t)w.K * w.ldb - w.n0) * 2);
-      issue_half(rs, vB[h - 2][0], vB[h - 2][1], k0 * (LB == LAY_KC ? 2 : (int)(w.ldb * 2)), dst, wave);
+      const rsrc_t rs = LB == LAY_KC ? make_rsrc(w.B + (int64_t)w.n0 * w.ldb * ESZ, ((int64_t)w.N - w.n0) * w.ldb * ESZ)
+                                     : make_rsrc(w.B + (int64_t)w.n0 * ESZ, ((int64_t)w.K * w.ldb - w.n0) * ESZ);
+      issue_half(rs, vB[h - 2][0], vB[h - 2][1], k0 * (LB == LAY_KC ? ESZ : (int)(w.ldb * ESZ)), dst, wave);
     }
   };
   // K-tile 0 whole + three halves of K-tile 1 (its Am1 follows in p0)
@@ -532,13 +588,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+      quad_mma<F8>(acc, 0, 0, fb[0], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p1: quadrant (0,1)
@@ -550,13 +600,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j][ks], fa[i][ks], acc[i][2 + j], 0, 0, 0);
+      quad_mma<F8>(acc, 0, 2, fb[1], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p2: quadrant (1,1)
@@ -568,14 +612,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 + i][2 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j][ks], fa[i][ks], acc[4 + i][2 + j], 0, 0, 0);
+      quad_mma<F8>(acc, 4, 2, fb[1], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p3: quadrant (1,0), operands already in VGPRs. Every LDS read of
@@ -596,13 +633,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       }
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
+      quad_mma<F8>(acc, 4, 0, fb[0], fa);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 || more1) SEG_BARRIER();   // group 1 skips its very last one (it took one extra up front)
     }
@@ -626,7 +657,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       epilogue4_slab(args.workspace + ((int64_t)z * args.splitk + blockIdx.y) * args.M * args.N, (int)args.M,
                      (int)args.N, args.alpha, acc, m0, n0, wm, wn, lane);
     } else {
-      epilogue4<OutT, EPI>(args, acc, z, m0, n0, wm, wn, lane);
+      epilogue4<OutT, EPI, F8 != 0>(args, acc, z, m0, n0, wm, wn, lane, sa, sb);
     }
     STAMP(3);
 #ifdef GEMM4_STAMPS
@@ -638,6 +669,17 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 template <int LA, int LB, typename OutT, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
   gemm4_body<LA, LB, OutT, EPI, SPLIT, false>(args, nullptr);
+}
+
+// fp8 operands (maeclip_gemm_fp8): KC x KC, per-row / per-column scales
+struct Gemm8Args {
+  maeclip_gemm_args a;
+  const float* sa;
+  const float* sb;
+};
+template <typename OutT, int EPI, int F8>
+__global__ void __launch_bounds__(512) gemm4_f8_kernel(const Gemm8Args g) {
+  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8>(g.a, nullptr, g.sa, g.sb);
 }
 
 // grouped weight gradients: RC x RC, fp32 out, no epilogue (beta only)
@@ -736,6 +778,75 @@ int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
   return out4<LAY_RC, LAY_RC>(a, s);
 }
 }  // namespace maeclip
+
+// ------------------------------------------------------------ fp8 operands
+namespace {
+
+template <typename OutT, int EPI, int F8>
+int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStream_t s) {
+  auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int tiles = (int)(((a.M + 255) / 256) * ((a.N + 255) / 256));
+  const int grid = (a.batch > 1 || tiles < ncu) ? tiles : ncu;
+  Gemm8Args g;
+  g.a = a;
+  g.sa = sa;
+  g.sb = sb;
+  hipLaunchKernelGGL(kern, dim3(grid, 1, (unsigned)a.batch), dim3(512), LDS_BYTES, s, g);
+  MC_CHECK_LAUNCH("maeclip_gemm_fp8");
+  return 0;
+}
+
+template <typename OutT, int F8>
+int epi_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStream_t s) {
+  switch (a.epilogue) {
+    case EPI_NONE: return launch_f8<OutT, EPI_NONE, F8>(a, sa, sb, s);
+    case EPI_GELU: return launch_f8<OutT, EPI_GELU, F8>(a, sa, sb, s);
+    case EPI_RESID: return launch_f8<OutT, EPI_RESID, F8>(a, sa, sb, s);
+    case EPI_GELU_D: return launch_f8<OutT, EPI_GELU_D, F8>(a, sa, sb, s);
+    case EPI_MUL_AUX: return launch_f8<OutT, EPI_MUL_AUX, F8>(a, sa, sb, s);
+    default: return launch_f8<OutT, EPI_DGELU, F8>(a, sa, sb, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int32_t maeclip_gemm_fp8(const maeclip_gemm_args* a, const float* scale_a, const float* scale_b,
+                                    void* stream) {
+  MC_CHECK_ARG(a != nullptr && scale_a != nullptr && scale_b != nullptr, "maeclip_gemm_fp8: null argument");
+  MC_CHECK_ARG(a->dtype == MAECLIP_FP8_E4M3 || a->dtype == MAECLIP_FP8_E5M2,
+               "maeclip_gemm_fp8: dtype (A format) must be MAECLIP_FP8_E4M3 or MAECLIP_FP8_E5M2");
+  MC_CHECK_ARG(a->a_layout == LAY_KC && a->b_layout == LAY_KC, "maeclip_gemm_fp8: KC x KC operands only");
+  MC_CHECK_ARG(a->K > 0 && a->K % 128 == 0, "maeclip_gemm_fp8: K=%lld must be a positive multiple of 128",
+               (long long)a->K);
+  MC_CHECK_ARG(a->M >= 256 && a->N >= 256 && a->N % 8 == 0, "maeclip_gemm_fp8: M, N >= 256 and N %% 8 == 0");
+  MC_CHECK_ARG(a->splitk <= 1, "maeclip_gemm_fp8: no split-K");
+  MC_CHECK_ARG(a->batch >= 1, "maeclip_gemm_fp8: batch >= 1");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  MC_CHECK_ARG(al16(a->A) && al16(a->B) && a->lda % 16 == 0 && a->ldb % 16 == 0 && a->lda >= a->K && a->ldb >= a->K,
+               "maeclip_gemm_fp8: operands need 16-B aligned rows (lda, ldb %% 16 == 0, >= K)");
+  MC_CHECK_ARG(al16(a->C) && (a->out_dtype == MAECLIP_BF16 ? a->ldc % 8 : a->ldc % 4) == 0 && al16(scale_b),
+               "maeclip_gemm_fp8: C / scale_b alignment");
+  const bool wa = a->epilogue == EPI_GELU || a->epilogue == EPI_GELU_D;
+  const bool ra = a->epilogue == EPI_DGELU || a->epilogue == EPI_MUL_AUX;
+  MC_CHECK_ARG(!(wa && a->aux_out && (!al16(a->aux_out) || a->ldaux % 8)) && !(ra && (!al16(a->aux) || a->ldaux % 8)),
+               "maeclip_gemm_fp8: aux alignment");
+  MC_CHECK_ARG(!a->resid || (al16(a->resid) && a->ldr % 4 == 0), "maeclip_gemm_fp8: resid alignment");
+  MC_CHECK_ARG(!a->bias || al16(a->bias), "maeclip_gemm_fp8: bias alignment");
+  const int64_t lim = 0x7fffffffLL;
+  MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "maeclip_gemm_fp8: operand exceeds 2^31 bytes");
+  hipStream_t s = (hipStream_t)stream;
+  const bool e5 = a->dtype == MAECLIP_FP8_E5M2;
+  if (a->out_dtype == MAECLIP_BF16)
+    return e5 ? epi_f8<bf16_t, 2>(*a, scale_a, scale_b, s) : epi_f8<bf16_t, 1>(*a, scale_a, scale_b, s);
+  return e5 ? epi_f8<float, 2>(*a, scale_a, scale_b, s) : epi_f8<float, 1>(*a, scale_a, scale_b, s);
+}
 
 // ------------------------------------------------- grouped weight gradients
 namespace {

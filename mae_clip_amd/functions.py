@@ -137,6 +137,25 @@ class StackSpec:
     wT: list                        # per block: (qkv, proj, fc1, fc2) weights in `dtype`
     side: bool = True               # weight gradients on the side stream (when not grouped)
     grouped_wgrad: bool = True      # one grouped launch for all weight gradients of the stack
+    w8: list = None                 # fp8 mode: per block ((W, W^T) fp8 operands) x (qkv, proj, fc1, fc2)
+
+
+def _fwd(x, w, w8, **kw):
+    """Forward GEMM of a stack: bf16 / fp32 (w), or fp8 (w8 = (W, W^T)): x is
+    quantised per token (e4m3) and multiplied with W (per output channel)."""
+    if w8 is None:
+        return K.linear_fwd(x, w, **kw)
+    kw.setdefault("out_dtype", x.dtype)
+    return K.linear_fp8(K.quant_rows_fp8(x, K.FP8_E4M3), w8[0], **kw)
+
+
+def _dgrad(dy, w, w8, **kw):
+    """dgrad GEMM dX = dY W: fp8 mode quantises dY per token (e5m2, the wider
+    range of gradients) and multiplies with W^T (per input channel)."""
+    if w8 is None:
+        return K.linear_dgrad(dy, w, **kw)
+    kw.setdefault("out_dtype", dy.dtype)
+    return K.linear_fp8(K.quant_rows_fp8(dy, K.FP8_E5M2), w8[1], **kw)
 
 
 PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
@@ -155,15 +174,16 @@ class TransformerStackFn(torch.autograd.Function):
         for i, (wqkv, wproj, w1, w2) in enumerate(spec.wT):
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
+            f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
             h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T)
-            qkv = K.linear_fwd(h1, wqkv, bqkv)
+            qkv = _fwd(h1, wqkv, f8[0], bias=bqkv)
             o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
-            x1 = K.linear_fwd(o, wproj, bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
+            x1 = _fwd(o, wproj, f8[1], bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
             h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T)
             # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
             dgelu = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
-            a = K.linear_fwd(h2, w1, b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
-            x2 = K.linear_fwd(a, w2, b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
+            a = _fwd(h2, w1, f8[2], bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
+            x2 = _fwd(a, w2, f8[3], bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
             saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a])
             xi = x2
         ctx.saved = saved
@@ -194,6 +214,7 @@ class TransformerStackFn(torch.autograd.Function):
             gT = g
         for i in reversed(range(len(spec.wT))):
             wqkv, wproj, w1, w2 = spec.wT[i]
+            f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n2w = p[0], p[6]
             xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
@@ -202,12 +223,12 @@ class TransformerStackFn(torch.autograd.Function):
             # mlp.fc2 (+ GELU backward fused into the dgrad epilogue: dA = (dy W2) * gelu'(h))
             gi[11] = rb.add(cpart, out=gout(ar, p[11]))
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
-            dA = K.linear_dgrad(gT, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
+            dA = _dgrad(gT, w2, f8[3], epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
             gi[10] = wq.wgrad(gT, a, out=gout(ar, p[10]))
             del a, dgelu
             # mlp.fc1
             gi[9] = rb.add(dA_part, out=gout(ar, p[9]))
-            dh2 = K.linear_dgrad(dA, w1)
+            dh2 = _dgrad(dA, w1, f8[2])
             gi[8] = wq.wgrad(dA, h2, out=gout(ar, p[8]))
             del dA
             # norm2 (+ residual gradient)
@@ -217,13 +238,13 @@ class TransformerStackFn(torch.autograd.Function):
                 dx1T = dx1
             # attn.proj
             gi[5] = rb.add(pc, out=gout(ar, p[5]))
-            dO = K.linear_dgrad(dx1T, wproj)
+            dO = _dgrad(dx1T, wproj, f8[1])
             gi[4] = wq.wgrad(dx1T, o, out=gout(ar, p[4]))
             # attention
             dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
             del dO
             gi[3] = rb.add(qpart, out=gout(ar, p[3]))
-            dh1 = K.linear_dgrad(dqkv, wqkv)
+            dh1 = _dgrad(dqkv, wqkv, f8[0])
             gi[2] = wq.wgrad(dqkv, h1, out=gout(ar, p[2]))
             del dqkv
             # norm1 (+ residual gradient)

@@ -84,6 +84,94 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
         LAUNCH_HOOK(key, 2.0 * M * N * K * batch, nbytes, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
 
 
+# ------------------------------------------------------------------ fp8
+FP8_E4M3, FP8_E5M2 = 2, 3     # MAECLIP_FP8_* (OCP e4m3fn / e5m2)
+
+
+class Fp8Rows:
+    """An fp8 GEMM operand: q uint8 [rows, cols] (OCP bytes) + per-row
+    dequantisation scales s f32 [rows] (x ~= s[r] * q[r, :])."""
+    __slots__ = ("q", "s", "fmt")
+
+    def __init__(self, q, s, fmt):
+        self.q, self.s, self.fmt = q, s, fmt
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+
+def quant_rows_fp8(x, fmt=FP8_E4M3, out=None):
+    """Row-wise fp8 quantisation of x [rows, cols] (bf16 / f32): one pass,
+    s = amax(row) / FMT_MAX."""
+    _dev(x)
+    rows, cols = x.shape
+    if out is None:
+        out = Fp8Rows(torch.empty((rows, cols), device=x.device, dtype=torch.uint8),
+                      torch.empty((rows,), device=x.device, dtype=torch.float32), fmt)
+    _call("maeclip_quant_rows_fp8", x.data_ptr(), _dt(x), rows, cols, x.stride(0), out.q.data_ptr(), out.q.stride(0),
+          out.s.data_ptr(), fmt, _stream())
+    return out
+
+
+def quant_cols_fp8(w, out=None):
+    """W^T quantised (e4m3) from the fp32 master W [rows, cols]: q [cols, rows],
+    one scale per column of W (= per row of W^T)."""
+    _dev(w)
+    rows, cols = w.shape
+    if w.dtype != torch.float32 or w.stride(1) != 1:
+        raise TypeError("quant_cols_fp8: fp32 row-major W")
+    if out is None:
+        ldq = (rows + 15) // 16 * 16
+        out = Fp8Rows(torch.empty((cols, ldq), device=w.device, dtype=torch.uint8)[:, :rows],
+                      torch.empty((cols,), device=w.device, dtype=torch.float32), FP8_E4M3)
+    nb = int(L.lib().maeclip_quant_cols_fp8_workspace(rows, cols))
+    ws = torch.empty((nb // 4,), device=w.device, dtype=torch.float32)
+    _call("maeclip_quant_cols_fp8", w.data_ptr(), rows, cols, w.stride(0), out.q.data_ptr(), out.q.stride(0),
+          out.s.data_ptr(), ws.data_ptr(), nb, _stream())
+    return out
+
+
+def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=None, aux=None, aux_out=None,
+             resid=None, colsum=None):
+    """Cout[M, N] = epilogue(alpha * (s_A[m] s_B[n]) * sum_k qA[m, k] qB[n, k]) on the
+    block-scaled fp8 MFMA (A e4m3 or e5m2, B e4m3; KC x KC, K % 128 == 0)."""
+    M, K = A.q.shape
+    N = B.q.shape[0]
+    if B.q.shape[1] != K or B.fmt != FP8_E4M3:
+        raise ValueError("gemm_fp8: B must be e4m3 [N, K] with A's K")
+    _dev(A.q, B.q, Cout, bias, aux, aux_out, resid, colsum)
+    a = L.GemmArgs(A=A.q.data_ptr(), B=B.q.data_ptr(), C=Cout.data_ptr(), M=M, N=N, K=K, lda=A.q.stride(0),
+                   ldb=B.q.stride(0), ldc=Cout.stride(0), batch=1, strideA=0, strideB=0, strideC=0,
+                   dtype=A.fmt, out_dtype=_dt(Cout), a_layout=KC, b_layout=KC, epilogue=epilogue,
+                   alpha=alpha, beta=0.0, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out),
+                   ldaux=(aux.stride(0) if aux is not None else aux_out.stride(0) if aux_out is not None else 0),
+                   resid=_ptr(resid), ldr=(resid.stride(0) if resid is not None else 0),
+                   colsum_partial=_ptr(colsum), splitk=1, workspace=None)
+    launch = lambda: _call("maeclip_gemm_fp8", C.byref(a), A.s.data_ptr(), B.s.data_ptr(), _stream())
+    if LAUNCH_HOOK is None:
+        launch()
+        return Cout
+    ec = Cout.element_size()
+    nbytes = M * K + N * K + M * N * ec
+    for t in (aux, aux_out):
+        if t is not None:
+            nbytes += M * N * t.element_size()
+    if resid is not None:
+        nbytes += M * N * 4
+    key = f"M{M} N{N} K{K} KK epi{epilogue} fp8{'e5' if A.fmt == FP8_E5M2 else 'e4'}>{'bf16' if ec == 2 else 'f32'}"
+    LAUNCH_HOOK(key, 2.0 * M * N * K, nbytes, launch)
+    return Cout
+
+
+def linear_fp8(xq: Fp8Rows, wq: Fp8Rows, bias=None, out_dtype=torch.bfloat16, epilogue=EPI_NONE, resid=None,
+               aux_out=None, aux=None, colsum=None):
+    """y[M, N] = x[M, K] w[N, K]^T on fp8 operands (forward: w = W [N_out, K_in];
+    dgrad: x = dY, w = W^T [K_in, N_out])."""
+    y = torch.empty((xq.q.shape[0], wq.q.shape[0]), device=xq.q.device, dtype=out_dtype)
+    return gemm_fp8(xq, wq, y, epilogue=epilogue, bias=bias, resid=resid, aux_out=aux_out, aux=aux, colsum=colsum)
+
+
 def gemm_colsum_rows(M: int) -> int:
     return int(L.lib().maeclip_gemm_colsum_rows(M))
 

@@ -37,11 +37,11 @@ VIT_SPECS = {
 
 def compute_dtype(precision=None) -> torch.dtype:
     precision = precision or CFG.precision
-    if precision == "bf16":
+    if precision in ("bf16", "fp8"):     # fp8: bf16 activations, fp8 transformer-stack GEMM operands
         return torch.bfloat16
     if precision == "fp32":
         return torch.float32
-    raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+    raise ValueError(f"precision must be 'bf16', 'fp8' or 'fp32', got {precision!r}")
 
 
 def _require_device(t: torch.Tensor, what: str):
@@ -56,14 +56,21 @@ def _trunc_normal_(t, std=0.02):
 
 class WeightCache:
     """bf16 shadows of the GEMM weights, refreshed by ONE multi-tensor cast
-    launch per forward (fp32 master weights stay the nn.Parameters)."""
+    launch per forward (fp32 master weights stay the nn.Parameters).
 
-    def __init__(self):
+    fp8=True (precision "fp8", C4): the transformer stacks' GEMM weights are
+    also quantised once per forward from their fp32 masters (get_fp8): W with
+    one e4m3 scale per output channel (forward GEMM B operand) and W^T with one
+    per input channel (dgrad GEMM B operand)."""
+
+    def __init__(self, fp8=False):
         self.entries = []    # (param, shape2d)
         self.views = {}
         self.key = None
         self.plan = None
         self.buf = None
+        self.fp8 = fp8
+        self.f8 = {}
 
     def register(self, p: torch.Tensor, shape2d):
         self.entries.append((p, tuple(shape2d)))
@@ -91,6 +98,18 @@ class WeightCache:
         if dtype == torch.float32:
             return p if shape2d is None else p.view(shape2d)
         return self.views[id(p)]
+
+    def get_fp8(self, p: torch.Tensor):
+        """(W, W^T) fp8 operands of GEMM weight p [N, K], quantised now (call
+        once per forward: the quantisation is part of the captured step)."""
+        w = p.detach()
+        prev = self.f8.get(id(p))
+        if prev is not None and prev[0].q.device != w.device:
+            prev = None
+        wq = K.quant_rows_fp8(w, K.FP8_E4M3, out=prev[0] if prev else None)
+        wt = K.quant_cols_fp8(w, out=prev[1] if prev else None)
+        self.f8[id(p)] = (wq, wt)
+        return wq, wt
 
 
 # ------------------------------------------------------------------ ViT
@@ -137,20 +156,23 @@ class Block(nn.Module):
             nn.init.zeros_(lin.bias)
 
 
-def run_stack(blocks, x, heads, dtype, cache: WeightCache, chunk=None):
+def run_stack(blocks, x, heads, dtype, cache: WeightCache, chunk=None, fp8=True):
     """The blocks as one TransformerStackFn, or as consecutive Functions of
     `chunk` blocks: autograd accumulates a Function's parameter gradients when
     its backward returns, so under data parallelism a chunked encoder hands its
     upper blocks' gradients to the bucketed all-reduce while the backward of the
     lower blocks is still running (the all-reduce of the last stack in the
-    backward is otherwise fully exposed)."""
+    backward is otherwise fully exposed). fp8=False keeps a stack on bf16 GEMMs
+    when the cache is in fp8 mode."""
     B, n, D = x.shape
     chunk = chunk or len(blocks)
     for c0 in range(0, len(blocks), chunk):
         part = blocks[c0:c0 + chunk]
         wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in part]
+        w8 = ([tuple(cache.get_fp8(w) for w in blk.gemm_weights()) for blk in part]
+              if fp8 and getattr(cache, "fp8", False) and dtype == torch.bfloat16 else None)
         spec = Fn.StackSpec(B=B, n=n, D=D, H=heads, eps=part[0].norm1.eps, dtype=dtype, wT=wT,
-                            side=bool(CFG.side_stream), grouped_wgrad=bool(CFG.wgrad_grouped))
+                            side=bool(CFG.side_stream), grouped_wgrad=bool(CFG.wgrad_grouped), w8=w8)
         params = [p for blk in part for p in blk.stack_params()]
         x = Fn.TransformerStackFn.apply(x, spec, *params)
     return x
@@ -237,7 +259,7 @@ class VisionTransformer(nn.Module):
         dtype = compute_dtype(self.precision)
         cache = getattr(self, "_cache", None)
         if cache is None:
-            cache = WeightCache()
+            cache = WeightCache(fp8=self.precision == "fp8")
             self.register_weights(cache)
             self._cache = cache
         cache.refresh(dtype)

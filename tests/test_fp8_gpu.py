@@ -1,0 +1,138 @@
+"""fp8 path (C4, BASELINE.json configs[4]): quantisation kernels bit-exact
+against torch's OCP float8 conversion, the block-scaled fp8 GEMM against an
+fp64 product of the dequantised operands, and the ViT-L/14@336 model in fp8
+against the CPU oracle and the bf16 path (documented tolerances)."""
+import pytest
+import torch
+
+from mae_clip_amd import kernels as K
+from tests.helpers import build_pair, make_batch
+
+pytestmark = pytest.mark.gpu
+
+F8 = {K.FP8_E4M3: (torch.float8_e4m3fn, 448.0), K.FP8_E5M2: (torch.float8_e5m2, 57344.0)}
+
+
+def _rows_input(rows, cols, dtype, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(rows, cols, generator=g) * torch.logspace(-6, 3, rows).view(-1, 1)
+    x[3] = 0.0                                   # amax 0 -> scale 1
+    x[5, 7] = 1e4                                # outlier row
+    return x.to(dtype).to(dev)
+
+
+def _ref_rows(x, fmt):
+    tdt, fmax = F8[fmt]
+    xf = x.float().cpu()
+    amax = xf.abs().amax(1)
+    s = torch.where(amax > 0, amax / fmax, torch.ones_like(amax))
+    q = (xf * (1.0 / s).view(-1, 1)).to(tdt)     # the kernel multiplies by 1/s, RNE
+    return q, s
+
+
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cols", [512, 1024, 4096, 5120])
+def test_quant_rows_bit_exact(dev, fmt, dtype, cols):
+    x = _rows_input(37, cols, dtype, dev, seed=cols)
+    out = K.quant_rows_fp8(x, fmt)
+    q_ref, s_ref = _ref_rows(x, fmt)
+    assert torch.equal(out.s.cpu(), s_ref)
+    assert torch.equal(out.q.cpu(), q_ref.view(torch.uint8))
+
+
+def test_quant_cols_bit_exact(dev):
+    g = torch.Generator().manual_seed(7)
+    w = (torch.randn(200, 136, generator=g) * torch.logspace(-3, 1, 136)).to(dev)
+    out = K.quant_cols_fp8(w)
+    q_ref, s_ref = _ref_rows(w.t().contiguous(), K.FP8_E4M3)
+    assert out.q.shape == (136, 200)
+    assert torch.equal(out.s.cpu(), s_ref)
+    assert torch.equal(out.q.cpu(), q_ref.view(torch.uint8))
+
+
+def _deq(op):
+    tdt = F8[op.fmt][0]
+    return op.q.cpu().view(tdt).double() * op.s.cpu().double().view(-1, 1)
+
+
+@pytest.mark.parametrize("afmt", [K.FP8_E4M3, K.FP8_E5M2])
+@pytest.mark.parametrize("mnk", [(512, 384, 256), (1000, 768, 1024), (2308, 512, 2048)])
+def test_gemm_fp8_vs_dequantised_fp64(dev, afmt, mnk):
+    """C = (s_A q_A)(s_B q_B)^T: the operands are exact in fp64, so the only
+    error is the fp32 accumulation (and the bf16 / fp32 output rounding)."""
+    M, N, Kd = mnk
+    g = torch.Generator().manual_seed(M + N)
+    x = (torch.randn(M, Kd, generator=g) * 3).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, Kd, generator=g) * 0.05).to(dev)
+    A = K.quant_rows_fp8(x, afmt)
+    B = K.quant_rows_fp8(w, K.FP8_E4M3)
+    ref = _deq(A) @ _deq(B).t()
+    bias = torch.randn(N, generator=g).to(dev)
+    y = K.linear_fp8(A, B, out_dtype=torch.float32)
+    sc = ref.abs().max().item()
+    tol = 5e-6 * Kd ** 0.5          # fp32 accumulation of exact products (+ the scale multiply)
+    assert (y.double().cpu() - ref).abs().max().item() / sc < tol
+    # epilogues of the stack: GELU' (bf16 out + aux), residual (fp32), mul-aux
+    d = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+    y4 = K.linear_fp8(A, B, bias=bias, epilogue=K.EPI_GELU_D, aux_out=d)
+    r64 = (ref + bias.double().cpu()).requires_grad_(True)
+    gl = torch.nn.functional.gelu(r64)
+    gd = torch.autograd.grad(gl.sum(), r64)[0]
+    assert (y4.double().cpu() - gl.detach()).abs().max().item() < 1e-2 * max(1.0, gl.abs().max().item())
+    assert (d.double().cpu() - gd).abs().max().item() < 2e-2
+    res = torch.randn(M, N, generator=g).to(dev)
+    y2 = K.linear_fp8(A, B, bias=bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=res)
+    assert (y2.double().cpu() - (ref + bias.double().cpu() + res.double().cpu())).abs().max().item() < tol * sc + 1e-5
+    aux = torch.rand(M, N, generator=g).to(torch.bfloat16).to(dev)
+    y5 = K.linear_fp8(A, B, epilogue=K.EPI_MUL_AUX, aux=aux)
+    ref5 = ref * aux.double().cpu()
+    assert (y5.double().cpu() - ref5).abs().max().item() < 1e-2 * ref5.abs().max().item()
+
+
+def test_fp8_quantisation_error_is_bounded(dev):
+    """e4m3 rows: |x - s q| <= 2^-4 |x| + s 2^-10 per element (3 mantissa bits,
+    RNE; subnormal step 2^-9 s) -- the operand error the fp8 GEMM adds."""
+    x = (torch.randn(64, 1024) * 2).to(torch.bfloat16).to(dev)
+    A = K.quant_rows_fp8(x, K.FP8_E4M3)
+    xd = _deq(A)
+    xr = x.double().cpu()
+    bound = 2.0 ** -4 * xr.abs() + A.s.cpu().double().view(-1, 1) * 2.0 ** -10
+    assert ((xd - xr).abs() <= bound + 1e-12).all()
+
+
+def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
+    """C4 shapes (ViT-L/14 @336, encoder cut to 4 blocks, B = 4; decoder 2 x 512,
+    n = 577): fp8 stack GEMMs (e4m3 forward, e5m2 x e4m3 dgrad, per-token /
+    per-channel scales) vs the fp64 CPU oracle on the same weights. Tolerances:
+    loss within 3e-2 relative (the bf16 path is held to 2e-2 by
+    test_vitl14_336_shapes_bf16_vs_oracle), and every trainable gradient within
+    relative L2 error 0.15 of the bf16 path's (e4m3 operands carry 3 mantissa
+    bits against bf16's 7)."""
+    kw = dict(model_name="vit_large_patch14_336", size=336, image_embedding=1024, text_layers=2, mask_ratio=0.75,
+              decoder_embed_dim=512, decoder_depth=2, decoder_num_heads=16, vit_depth=4)
+    batch = make_batch(4, 336)
+    out = {}
+    for prec in ("fp8", "bf16"):
+        prod, ref = build_pair(prec, **kw)
+        prod.eval()
+        loss = prod({k: v.to(dev) for k, v in batch.items()})
+        loss.backward()
+        torch.cuda.synchronize()
+        out[prec] = (loss.item(), {n: p.grad.detach().double().cpu() for n, p in prod.named_parameters()
+                                   if p.requires_grad})
+    ref.eval()
+    with torch.no_grad():
+        rloss = ref(dict(batch, image=batch["image"].double())).item()
+    l8, g8 = out["fp8"]
+    lb, gb = out["bf16"]
+    print(f"fp8 loss {l8:.6f}  bf16 loss {lb:.6f}  oracle {rloss:.6f}")
+    assert abs(l8 - rloss) < 3e-2 * max(1.0, abs(rloss)), (l8, lb, rloss)
+    worst = 0.0
+    for n, gbn in gb.items():
+        assert torch.isfinite(g8[n]).all(), n
+        den = gbn.norm().item()
+        if den > 0:
+            worst = max(worst, (g8[n] - gbn).norm().item() / den)
+    print(f"worst relative L2 gradient deviation fp8 vs bf16: {worst:.4f}")
+    assert worst < 0.15, worst
