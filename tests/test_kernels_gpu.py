@@ -502,3 +502,4 @@ def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
     assert torch.equal(dy2.float().view(B, keep + 1, Dd).cpu(), ref_dy.float().to(dtype).float())
     assert (dmask.double().cpu().sum(0) - ref_dm).abs().max().item() < 1e-3
     assert (cs.double().cpu().sum(0) - ref_dy.sum((0, 1))).abs().max().item() < 1e-3
+

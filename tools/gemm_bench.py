@@ -47,7 +47,11 @@ if os.environ.get("GEMM_SET") == "epi":   # production epilogues (functions.py),
               ("dec fc2 fwd +res", D, 512, 2048, 0, 0, 2), ("enc fc2 fwd +res", E, 768, 3072, 0, 0, 2),
               ("dec proj fwd +res", D, 512, 512, 0, 0, 2), ("enc proj fwd +res", E, 768, 768, 0, 0, 2),
               ("dec proj dgrad", D, 512, 512, 0, 1, 0), ("enc proj dgrad", E, 768, 768, 0, 1, 0),
-              ("dec qkv dgrad", D, 512, 1536, 0, 1, 0), ("enc qkv dgrad", E, 768, 2304, 0, 1, 0)]
+              ("dec qkv dgrad", D, 512, 1536, 0, 1, 0), ("enc qkv dgrad", E, 768, 2304, 0, 1, 0),
+              ("enc fc1 dgrad", E, 768, 3072, 0, 1, 0), ("dec fc1 dgrad", D, 512, 2048, 0, 1, 0),
+              ("enc qkv fwd", E, 2304, 768, 0, 0, 0), ("dec qkv fwd", D, 1536, 512, 0, 0, 0),
+              ("L enc fc2 fwd +res", 128 * 145, 1024, 4096, 0, 0, 2), ("L enc qkv fwd", 128 * 145, 3072, 1024, 0, 0, 0),
+              ("L enc fc1 dgrad", 128 * 145, 1024, 4096, 0, 1, 0)]
 
 
 def epi_kwargs(epi, M, N):
