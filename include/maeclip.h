@@ -310,6 +310,25 @@ typedef struct {
   float max_pixel;
 } maeclip_image_u8_args;
 int32_t maeclip_image_normalize_u8(const maeclip_image_u8_args* args, void* stream);
+/* The whole get_transforms() pipeline of dataset.py:44-58 + the permute of
+ * :34 in one pass, for decoded RGB uint8 HWC images of ANY sizes: A.Resize(S,
+ * S) (cv2.resize INTER_LINEAR: OpenCV's fixed-point uint8 algorithm, equal
+ * size = copy, exact 2x = INTER_AREA) then A.Normalize as above, into dst fp32
+ * [B][3][S][S]. images: DEVICE array of B descriptors (src rows of row_stride
+ * bytes, 3 interleaved channels). */
+typedef struct {
+  const uint8_t* src;
+  int32_t H, W;
+  int64_t row_stride;
+} maeclip_image_src;
+typedef struct {
+  const maeclip_image_src* images;
+  float* dst;
+  int64_t B, S;
+  float mean[3], std[3];
+  float max_pixel;
+} maeclip_preprocess_args;
+int32_t maeclip_image_preprocess_u8(const maeclip_preprocess_args* args, void* stream);
 
 /* Retrieval (inference.py:40-45). l2_normalize replaces F.normalize(x, p=2,
  * dim=-1): y = x / max(||x||_2, eps), fp32 [M][P] rows (strides ldx / ldy).

@@ -112,6 +112,15 @@ class WgradProblem(C.Structure):
     _fields_ = [("dy", c_vp), ("x", c_vp), ("dw", c_vp), ("N", c_i64), ("K", c_i64), ("ldy", c_i64), ("ldx", c_i64)]
 
 
+class ImageSrc(C.Structure):
+    _fields_ = [("src", c_vp), ("H", c_i32), ("W", c_i32), ("row_stride", c_i64)]
+
+
+class PreprocessArgs(C.Structure):
+    _fields_ = [("images", c_vp), ("dst", c_vp), ("B", c_i64), ("S", c_i64),
+                ("mean", c_f32 * 3), ("std", c_f32 * 3), ("max_pixel", c_f32)]
+
+
 class ImageU8Args(C.Structure):
     _fields_ = [("src", c_vp), ("dst", c_vp), ("B", c_i64), ("H", c_i64), ("W", c_i64),
                 ("mean", c_f32 * 3), ("std", c_f32 * 3), ("max_pixel", c_f32)]
@@ -133,6 +142,7 @@ _SIGS = {
     "maeclip_wgrad_grouped_workspace": (c_i64, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32]),
     "maeclip_wgrad_grouped": (c_i32, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32, c_f32, c_vp, c_i64, c_vp]),
     "maeclip_image_normalize_u8": (c_i32, [C.POINTER(ImageU8Args), c_vp]),
+    "maeclip_image_preprocess_u8": (c_i32, [C.POINTER(PreprocessArgs), c_vp]),
     "maeclip_l2_normalize": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f32, c_vp]),
     "maeclip_topk_rows": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "maeclip_attn_fwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),

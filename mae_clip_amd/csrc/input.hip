@@ -7,6 +7,11 @@
 // uploaded as uint8 (a quarter of the fp32 bytes over PCIe) and normalised
 // here, in HBM, straight into the model's NCHW fp32 input.
 //
+// maeclip_image_preprocess_u8 adds the resize in the same pass: images of any
+// size (one descriptor each) -> A.Resize(S, S) = cv2.resize INTER_LINEAR
+// (dataset.py:48; OpenCV's fixed-point uint8 algorithm, see oracle/input_ref.py)
+// -> Normalize -> NCHW fp32 [B, 3, S, S]: the whole get_transforms() pipeline.
+//
 // Arithmetic is albumentations' normalize(): mean32 = f32(mean) * max_pixel,
 // den32 = 1 / (f32(std) * max_pixel) (both fp32, computed on the host with
 // IEEE division), out = (f32(x) - mean32) * den32 -- two roundings, no FMA.
@@ -57,7 +62,85 @@ __global__ void __launch_bounds__(NTH) normalize_u8_kernel(const uint8_t* __rest
     dst[(b * 3 + c) * HW + off] = __fmul_rn(x, k.d[c]);
   }
 }
+// OpenCV INTER_LINEAR source index / fixed-point weights of output coordinate d
+// (resize.cpp, CV_8U: float f from double arithmetic, weights
+// saturate_cast<short>(w * 2048) = rint, borders clamp with weight 0)
+struct Lin {
+  int s0, s1, a0, a1;
+};
+__device__ __forceinline__ Lin lin_coef(int d, int n_src, int n_dst) {
+  const double scale = 1.0 / ((double)n_dst / (double)n_src);
+  float f = (float)((d + 0.5) * scale - 0.5);
+  int s = (int)floorf(f);
+  f -= (float)s;
+  bool hi = false;
+  if (s < 0) { s = 0; f = 0.f; }
+  if (s >= n_src - 1) { s = n_src - 1; f = 0.f; hi = true; }
+  Lin r;
+  r.s0 = s;
+  r.s1 = min(s + 1, n_src - 1);
+  r.a0 = (int)rintf((1.f - f) * 2048.f);
+  r.a1 = hi ? 0 : (int)rintf(f * 2048.f);
+  return r;
+}
+
+// one output pixel (3 channels) per thread; grid (pixel blocks, image)
+__global__ void __launch_bounds__(NTH) preprocess_u8_kernel(const maeclip_image_src* __restrict__ imgs, float* __restrict__ dst,
+                                                             int S, NormConst k) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * NTH + threadIdx.x;
+  if (p >= S * S) return;
+  const int dy = p / S, dx = p % S;
+  const maeclip_image_src im = imgs[b];
+  const uint8_t* src = im.src;
+  const int H = im.H, W = im.W;
+  const int64_t rs = im.row_stride;
+  int v[3];
+  if (H == S && W == S) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = src[dy * rs + dx * 3 + c];
+  } else if (H == 2 * S && W == 2 * S) {   // cv2: exact 2x -> INTER_AREA fast path
+    const uint8_t* r0 = src + (int64_t)(2 * dy) * rs + 2 * dx * 3;
+    const uint8_t* r1 = r0 + rs;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = (r0[c] + r0[3 + c] + r1[c] + r1[3 + c] + 2) >> 2;
+  } else {
+    const Lin x = lin_coef(dx, W, S), y = lin_coef(dy, H, S);
+    const uint8_t* r0 = src + (int64_t)y.s0 * rs;
+    const uint8_t* r1 = src + (int64_t)y.s1 * rs;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int h0 = r0[x.s0 * 3 + c] * x.a0 + r0[x.s1 * 3 + c] * x.a1;
+      const int h1 = r1[x.s0 * 3 + c] * x.a0 + r1[x.s1 * 3 + c] * x.a1;
+      // VResizeLinearVec_32s8u: mul_hi of (h >> 4) by the int16 weight, round by 2 bits
+      const int t = (((h0 >> 4) * y.a0) >> 16) + (((h1 >> 4) * y.a1) >> 16);
+      v[c] = min(max((t + 2) >> 2, 0), 255);
+    }
+  }
+  const int64_t plane = (int64_t)S * S;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dst[((int64_t)b * 3 + c) * plane + p] = __fmul_rn((float)v[c] - k.m[c], k.d[c]);
+}
 }  // namespace
+
+extern "C" int32_t maeclip_image_preprocess_u8(const maeclip_preprocess_args* a, void* stream) {
+  MC_CHECK_ARG(a && a->images && a->dst, "maeclip_image_preprocess_u8: null pointer");
+  MC_CHECK_ARG(a->B >= 0 && a->S > 0 && a->S <= 8192 && a->B <= 65535, "maeclip_image_preprocess_u8: bad sizes");
+  MC_CHECK_ARG(a->max_pixel > 0.f, "maeclip_image_preprocess_u8: max_pixel must be > 0");
+  NormConst k;
+  for (int c = 0; c < 3; ++c) {
+    MC_CHECK_ARG(a->std[c] > 0.f, "maeclip_image_preprocess_u8: std must be > 0");
+    k.m[c] = a->mean[c] * a->max_pixel;
+    const volatile float sd = a->std[c] * a->max_pixel;
+    k.d[c] = 1.0f / sd;
+  }
+  if (a->B == 0) return 0;
+  const int S = (int)a->S;
+  hipLaunchKernelGGL(preprocess_u8_kernel, dim3((unsigned)((S * S + NTH - 1) / NTH), (unsigned)a->B), dim3(NTH), 0,
+                     (hipStream_t)stream, a->images, a->dst, S, k);
+  MC_CHECK_LAUNCH("maeclip_image_preprocess_u8");
+  return 0;
+}
 
 extern "C" int32_t maeclip_image_normalize_u8(const maeclip_image_u8_args* a, void* stream) {
   MC_CHECK_ARG(a && a->src && a->dst, "maeclip_image_normalize_u8: null pointer");

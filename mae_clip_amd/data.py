@@ -3,10 +3,13 @@
 The reference's CLIPDataset.__getitem__ (dataset.py:24-37) decodes each image
 with cv2 (BGR -> RGB), runs albumentations Resize + Normalize
 (get_transforms, dataset.py:44-58) and permutes HWC -> CHW float32 on the host;
-main.py:55 then copies the fp32 batch to the GPU. Here decoding and resizing
-stay on the host (cv2 / PIL, unchanged), the batch crosses PCIe as uint8 HWC
-(4x fewer bytes) and libmaeclip normalises + transposes it in HBM
-(maeclip_image_normalize_u8), producing exactly the tensor the model takes.
+main.py:55 then copies the fp32 batch to the GPU. Here decoding stays on the
+host (cv2 / PIL, unchanged); the decoded uint8 HWC images cross PCIe as they
+are (any sizes, 4x fewer bytes than the fp32 batch), and libmaeclip resizes,
+normalises and transposes them in HBM in one pass
+(maeclip_image_preprocess_u8 = Resize + Normalize + permute), producing
+exactly the tensor the model takes. normalize_u8 is the resize-free variant
+for batches already at the model's size.
 """
 from __future__ import annotations
 
@@ -39,6 +42,34 @@ def normalize_u8(images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, max
     a = L.ImageU8Args(src=images.data_ptr(), dst=out.data_ptr(), B=B, H=H, W=W,
                       mean=(C.c_float * 3)(*mean), std=(C.c_float * 3)(*std), max_pixel=max_pixel_value)
     _call("maeclip_image_normalize_u8", C.byref(a), _stream())
+    return out
+
+
+def preprocess_images(images, size, mean=IMAGENET_MEAN, std=IMAGENET_STD, max_pixel_value=255.0, out=None):
+    """get_transforms() of dataset.py:44-58 (+ the permute of :34) on the device:
+    a list of uint8 HWC RGB images of any sizes (device tensors; row-strided
+    views allowed) -> float32 [B, 3, size, size]: A.Resize(size, size) with
+    cv2.INTER_LINEAR semantics, then A.Normalize."""
+    if not images:
+        raise ValueError("preprocess_images: empty image list")
+    dev = images[0].device
+    descs = (L.ImageSrc * len(images))()
+    for i, im in enumerate(images):
+        _dev(im)
+        if im.dtype != torch.uint8 or im.dim() != 3 or im.shape[2] != 3 or im.stride(2) != 1 or im.stride(1) != 3:
+            raise ValueError(f"preprocess_images: image {i} must be uint8 [H, W, 3] with packed pixels")
+        if im.device != dev:
+            raise ValueError("preprocess_images: images on different devices")
+        descs[i].src, descs[i].H, descs[i].W, descs[i].row_stride = im.data_ptr(), im.shape[0], im.shape[1], im.stride(0)
+    B = len(images)
+    if out is None:
+        out = torch.empty((B, 3, size, size), device=dev, dtype=torch.float32)
+    elif out.shape != (B, 3, size, size) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("preprocess_images: out must be a dense float32 [B, 3, size, size]")
+    d = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    a = L.PreprocessArgs(images=d.data_ptr(), dst=out.data_ptr(), B=B, S=size, mean=(C.c_float * 3)(*mean),
+                         std=(C.c_float * 3)(*std), max_pixel=max_pixel_value)
+    _call("maeclip_image_preprocess_u8", C.byref(a), _stream())
     return out
 
 

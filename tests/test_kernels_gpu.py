@@ -503,3 +503,25 @@ def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
     assert (dmask.double().cpu().sum(0) - ref_dm).abs().max().item() < 1e-3
     assert (cs.double().cpu().sum(0) - ref_dy.sum((0, 1))).abs().max().item() < 1e-3
 
+
+
+def test_image_preprocess_resize_bit_exact(dev):
+    """maeclip_image_preprocess_u8 (A.Resize INTER_LINEAR + A.Normalize +
+    permute, dataset.py:44-58 / :34) vs the numpy restatement of OpenCV's
+    fixed-point uint8 resize (oracle/input_ref.py): bit-exact fp32 output for
+    up- and down-scales, non-square and odd sizes, the equal-size copy, the exact
+    2x INTER_AREA case and a row-strided (cropped) source."""
+    import numpy as np
+    from mae_clip_amd.data import preprocess_images
+    from oracle.input_ref import preprocess_ref
+    rng = np.random.default_rng(5)
+    S = 224
+    shapes = [(375, 500), (224, 224), (448, 448), (100, 37), (1, 1), (225, 223), (640, 427)]
+    ims = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in shapes]
+    big = torch.from_numpy(rng.integers(0, 256, (300, 400, 3), dtype=np.uint8)).to(dev)
+    crop = big[10:260, 20:330]                      # row stride 1200 B, not 3 * 310
+    dev_ims = [torch.from_numpy(im).to(dev) for im in ims] + [crop]
+    out = preprocess_images(dev_ims, S).cpu().numpy()
+    ref = preprocess_ref(ims + [crop.cpu().numpy()], S)
+    assert out.shape == (len(dev_ims), 3, S, S)
+    assert np.array_equal(out, ref)

@@ -256,3 +256,23 @@ def test_clip_model_vs_reference(tag):
             close(named[k].grad, ref, rtol=1e-4)
             checked += 1
     assert checked >= 25, checked
+
+
+def test_resize_oracle_properties():
+    """The OpenCV INTER_LINEAR restatement (oracle/input_ref.py; opencv is
+    absent: parity unpinned) on cases with a known answer: constant images stay
+    constant at any scale, equal size copies, exact 2x downscale is the rounded
+    2x2 mean, and a 2x upscale of a horizontal ramp is monotone."""
+    import numpy as np
+    from oracle.input_ref import resize_u8_linear_ref
+    c = np.full((37, 53, 3), 201, np.uint8)
+    for s in (7, 32, 224):
+        assert np.all(resize_u8_linear_ref(c, s) == 201)
+    im = np.random.default_rng(0).integers(0, 256, (16, 16, 3), dtype=np.uint8)
+    assert np.array_equal(resize_u8_linear_ref(im, 16), im)
+    d = resize_u8_linear_ref(im, 8).astype(int)
+    i = im.astype(int)
+    assert np.array_equal(d, (i[0::2, 0::2] + i[0::2, 1::2] + i[1::2, 0::2] + i[1::2, 1::2] + 2) >> 2)
+    ramp = np.tile(np.arange(0, 256, 16, dtype=np.uint8)[None, :, None], (16, 1, 3))
+    up = resize_u8_linear_ref(ramp, 32).astype(int)
+    assert np.all(np.diff(up[0, :, 0]) >= 0) and up[0, 0, 0] == 0 and up[0, -1, 0] == 240
