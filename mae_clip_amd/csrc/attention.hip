@@ -393,7 +393,11 @@ __device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane
 // SDS (bf16 only, when the n x n image fits beside Q, K, V, dO): phase 1
 // keeps dS in LDS and phase 2 reads it back instead of recomputing S, dP and
 // the exponentials (the exp/VALU work bounds the hd = 32 decoder layers).
-template <typename T, int HD, bool SDS>
+// TWO_ (bf16; always on for fp32): two [npad][HD] images in LDS instead of four --
+// phase 1 keeps Q, dO and reads each wave's K/V tile from HBM, phase 2 reloads
+// the slots with K, V. Chosen when it fits more workgroups per CU (C4: decoder
+// n = 577, encoder n = 145 at HD = 64).
+template <typename T, int HD, bool SDS, bool TWO_ = false>
 __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
@@ -405,7 +409,8 @@ __global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_
   // as wide) holds two at a time so that n = 197 at HD = 64 fits: phase 1
   // keeps Q, dO in LDS and reads each wave's K/V tile from HBM, phase 2
   // reloads the two slots with K, V and reads Q/dO tiles from HBM.
-  constexpr bool TWO = !std::is_same<T, bf16_t>::value;
+  constexpr bool TWO = TWO_ || !std::is_same<T, bf16_t>::value;
+  static_assert(!(SDS && TWO), "dS-in-LDS needs the four-image layout");
   const int img = npad * I::ROWB;
   char* Qi = smem;
   char* Di = smem + (TWO ? 1 : 3) * img;
@@ -621,18 +626,48 @@ template <typename T, int HD> size_t fwd_lds(int n) {
   const int npad = (n + 63) & ~63;
   return (size_t)2 * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
 }
-template <typename T, int HD> size_t bwd_lds(int n, int nw) {
+template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   const int npad = (n + 31) & ~31;
-  const int nimg = std::is_same<T, bf16_t>::value ? 4 : 2;
+  const int nimg = (std::is_same<T, bf16_t>::value && !two) ? 4 : 2;
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
-template <typename T, int HD, bool SDS>
+template <typename T, int HD, bool SDS, bool TWO = false>
 void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS>), grid, dim3(nthreads), lds, s, a);
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO>), grid, dim3(nthreads), lds, s, a);
+}
+
+// resident workgroups per CU of a bwd variant (registers, waves and LDS)
+template <typename T, int HD, bool TWO>
+int bwd_occupancy(int nthreads, size_t lds) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, false, TWO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)attn_bwd_kernel<T, HD, false, TWO>, nthreads,
+                                                   lds) != hipSuccess)
+    return 0;
+  return nb;
+}
+
+// bf16: use the two-image backward when it keeps more workgroups per CU
+// resident (MAECLIP_ATTN_TWO=0 / 1 forces it off / on); cached per shape.
+template <int HD>
+bool bwd_two(int n, int nw, size_t lds4, size_t lds2) {
+  const char* e = getenv("MAECLIP_ATTN_TWO");
+  if (e && *e) return *e != '0';
+  static int cache[2][64][MAXW + 1] = {};   // (npad / 32) x nw -> 1 no, 2 yes
+  const int key = ((n + 31) >> 5) & 63;
+  int& c = cache[HD == 64][key][nw];
+  if (c == 0) {
+    const int occ4 = lds4 <= 163840 ? bwd_occupancy<bf16_t, HD, false>(64 * nw, lds4) : 0;
+    const int occ2 = bwd_occupancy<bf16_t, HD, true>(64 * nw, lds2);
+    c = occ2 > occ4 ? 2 : 1;
+  }
+  return c == 2;
 }
 
 template <typename T, int HD>
@@ -642,6 +677,14 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   const int nw = tiles < MAXW ? tiles : MAXW;
   const int nthreads = 64 * nw;
   size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
+  bool two = false;
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    if (bwd) {
+      const size_t lds2 = bwd_lds<T, HD>(a.n, nw, true);
+      two = bwd_two<HD>(a.n, nw, lds, lds2) && lds2 <= 163840;
+      if (two) lds = lds2;
+    }
+  }
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   dim3 grid((unsigned)(a.B * a.H));
   if (bwd) {
@@ -653,10 +696,11 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     const size_t lds_sds = lds + npad * npad * 2;
     bool sds = false;
     if constexpr (std::is_same<T, bf16_t>::value) {
-      sds = lds_sds <= 163840 && getenv_flag("MAECLIP_ATTN_SDS");
+      sds = !two && lds_sds <= 163840 && getenv_flag("MAECLIP_ATTN_SDS");
       if (sds) launch_bwd<T, HD, true>(a, grid, nthreads, lds_sds, s);
+      else if (two) launch_bwd<T, HD, false, true>(a, grid, nthreads, lds, s);
     }
-    if (!sds) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
+    if (!sds && !two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);

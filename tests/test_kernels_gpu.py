@@ -95,15 +95,22 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
-@pytest.mark.parametrize("sds", [True, False])
+@pytest.mark.parametrize("mode", ["four", "two", "sds"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
-                                   (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32)])
-def test_attention_fwd_bwd(dev, dtype, shape, sds, monkeypatch):
+                                   (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32), (1, 577, 2, 32),
+                                   (2, 145, 2, 64)])
+def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     """fp32 parity mode holds two [n][hd] f32 images at a time in the
-    backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well."""
+    backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well. bf16
+    backward variants: four LDS images ("four"), two images with K/V (phase 1)
+    and Q/dO (phase 2) tiles from HBM ("two", picked when it fits more
+    workgroups per CU), dS kept in LDS between the phases ("sds", opt-in)."""
     B, n, H, hd = shape
-    if sds:
+    if dtype == torch.float32 and (n > 256 or mode != "four"):
+        pytest.skip("fp32 parity mode: n <= 256, one variant")
+    monkeypatch.setenv("MAECLIP_ATTN_TWO", "1" if mode == "two" else "0")
+    if mode == "sds":
         # bf16 backward keeps dS in LDS for dQ instead of recomputing S/dP (opt-in)
         monkeypatch.setenv("MAECLIP_ATTN_SDS", "1")
     scale = hd ** -0.5
