@@ -397,8 +397,12 @@ __device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane
 // phase 1 keeps Q, dO and reads each wave's K/V tile from HBM, phase 2 reloads
 // the slots with K, V. Chosen when it fits more workgroups per CU (C4: decoder
 // n = 577, encoder n = 145 at HD = 64).
-template <typename T, int HD, bool SDS, bool TWO_ = false>
-__global__ void __launch_bounds__(MAXW * 64) attn_bwd_kernel(const maeclip_attn_args a) {
+// OCC > 1 asks the compiler for that many resident 8-wave workgroups per CU
+// (register budget 512 / (2 OCC)); used with TWO_ at HD = 32, where the
+// two-image LDS footprint would allow three.
+template <typename T, int HD, bool SDS, bool TWO_ = false, int OCC = 1>
+__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(2 * OCC)))
+attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
@@ -632,42 +636,44 @@ template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
-template <typename T, int HD, bool SDS, bool TWO = false>
+template <typename T, int HD, bool SDS, bool TWO = false, int OCC = 1>
 void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO, OCC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO>), grid, dim3(nthreads), lds, s, a);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO, OCC>), grid, dim3(nthreads), lds, s, a);
 }
 
 // resident workgroups per CU of a bwd variant (registers, waves and LDS)
-template <typename T, int HD, bool TWO>
+template <typename T, int HD, bool TWO, int OCC = 1>
 int bwd_occupancy(int nthreads, size_t lds) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, false, TWO>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, false, TWO, OCC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)attn_bwd_kernel<T, HD, false, TWO>, nthreads,
-                                                   lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)attn_bwd_kernel<T, HD, false, TWO, OCC>,
+                                                   nthreads, lds) != hipSuccess)
     return 0;
   return nb;
 }
 
 // bf16: use the two-image backward when it keeps more workgroups per CU
 // resident (MAECLIP_ATTN_TWO=0 / 1 forces it off / on); cached per shape.
+// returns 0 (four images), 1 (two images) or 3 (two images, 3 workgroups / CU)
 template <int HD>
-bool bwd_two(int n, int nw, size_t lds4, size_t lds2) {
+int bwd_two(int n, int nw, size_t lds4, size_t lds2) {
   const char* e = getenv("MAECLIP_ATTN_TWO");
-  if (e && *e) return *e != '0';
-  static int cache[2][64][MAXW + 1] = {};   // (npad / 32) x nw -> 1 no, 2 yes
+  if (e && *e) return *e == '0' ? 0 : *e == '3' && HD == 32 ? 3 : 1;
+  static int cache[2][64][MAXW + 1] = {};   // (npad / 32) x nw -> variant + 1
   const int key = ((n + 31) >> 5) & 63;
   int& c = cache[HD == 64][key][nw];
   if (c == 0) {
     const int occ4 = lds4 <= 163840 ? bwd_occupancy<bf16_t, HD, false>(64 * nw, lds4) : 0;
     const int occ2 = bwd_occupancy<bf16_t, HD, true>(64 * nw, lds2);
-    c = occ2 > occ4 ? 2 : 1;
+    const int occ3 = HD == 32 ? bwd_occupancy<bf16_t, HD, true, 3>(64 * nw, lds2) : 0;
+    c = occ3 > occ2 && occ3 > occ4 ? 4 : occ2 > occ4 ? 2 : 1;
   }
-  return c == 2;
+  return c - 1;
 }
 
 template <typename T, int HD>
@@ -678,10 +684,12 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   const int nthreads = 64 * nw;
   size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
   bool two = false;
+  int variant = 0;
   if constexpr (std::is_same<T, bf16_t>::value) {
     if (bwd) {
       const size_t lds2 = bwd_lds<T, HD>(a.n, nw, true);
-      two = bwd_two<HD>(a.n, nw, lds, lds2) && lds2 <= 163840;
+      variant = lds2 <= 163840 ? bwd_two<HD>(a.n, nw, lds, lds2) : 0;
+      two = variant != 0;
       if (two) lds = lds2;
     }
   }
@@ -698,6 +706,7 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     if constexpr (std::is_same<T, bf16_t>::value) {
       sds = !two && lds_sds <= 163840 && getenv_flag("MAECLIP_ATTN_SDS");
       if (sds) launch_bwd<T, HD, true>(a, grid, nthreads, lds_sds, s);
+      else if (variant == 3) launch_bwd<T, HD, false, true, HD == 32 ? 3 : 1>(a, grid, nthreads, lds, s);
       else if (two) launch_bwd<T, HD, false, true>(a, grid, nthreads, lds, s);
     }
     if (!sds && !two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
