@@ -55,3 +55,32 @@ def test_extended_checkpoint_restores_optimizer_and_step(tmp_path):
         assert torch.equal(sa[k]["exp_avg"], sb[k]["exp_avg"])
         assert torch.equal(sa[k]["exp_avg_sq"], sb[k]["exp_avg_sq"])
     assert torch.load(path, weights_only=True)["extra"] == {"epoch": 3}
+
+
+def test_reference_clip_only_state_dict_into_mae_model(tmp_path):
+    """A reference best.pt comes from the CLIP-only model (no MAE head): loading
+    it into an MAE model needs strict="reference", which tolerates exactly the
+    missing mae_decoder.* keys (reported) and nothing else."""
+    import pytest
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.checkpoint import load_checkpoint
+    kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    with product_config(**dict(kw, mask_ratio=0.0)):
+        torch.manual_seed(1)
+        ref_like = CLIPModel()
+    path = tmp_path / "best.pt"
+    torch.save(ref_like.state_dict(), path)
+    mae = _model()
+    with pytest.raises(RuntimeError):
+        load_checkpoint(path, mae)                       # strict: the decoder keys are missing
+    missing = []
+    assert load_checkpoint(path, mae, strict="reference", missing_out=missing) == 0
+    assert missing and all(k.startswith("mae_decoder.") for k in missing)
+    sd = mae.state_dict()
+    for k, v in ref_like.state_dict().items():
+        assert torch.equal(sd[k], v), k
+    bad = dict(ref_like.state_dict())
+    bad.pop("image_projection.fc.weight")
+    torch.save(bad, path)
+    with pytest.raises(RuntimeError):
+        load_checkpoint(path, _model(), strict="reference")
