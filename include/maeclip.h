@@ -99,6 +99,24 @@ int32_t maeclip_quant_rows_fp8(const void* x, int32_t x_dtype, int64_t rows, int
                                int64_t ldq, float* scales, int32_t fmt, void* stream);
 /* W^T quantisation (e4m3) from the fp32 master W [rows, ld]: qt [cols, ldq]
  * (ldq % 16 == 0), one scale per column of W (per row of W^T). */
+/* Every fp8 stack weight of a step at once (three launches): for each entry,
+ * q = rows of W quantised per output channel (scales sq [rows]) and qt = W^T
+ * quantised per input channel (scales sqt [cols], rows of ldqt bytes), from
+ * the fp32 master W [rows, ld]. The host array is filled in by
+ * maeclip_quant_weights_fp8_prepare (prefix sums; returns the workspace
+ * bytes); dev is its device copy. */
+typedef struct {
+  const float* w;
+  void* q;
+  float* sq;
+  void* qt;
+  float* sqt;
+  int32_t rows, cols, ld, ldqt;
+  int64_t row_begin, unit_begin, part_begin;
+} maeclip_fp8w_entry;
+int64_t maeclip_quant_weights_fp8_prepare(maeclip_fp8w_entry* host, int32_t n);
+int32_t maeclip_quant_weights_fp8(const maeclip_fp8w_entry* dev, const maeclip_fp8w_entry* host, int32_t n,
+                                  float* workspace, int64_t ws_bytes, void* stream);
 int64_t maeclip_quant_cols_fp8_workspace(int64_t rows, int64_t cols);
 int32_t maeclip_quant_cols_fp8(const float* w, int64_t rows, int64_t cols, int64_t ld, void* qt, int64_t ldq,
                                float* scales, float* workspace, int64_t ws_bytes, void* stream);

@@ -112,6 +112,12 @@ class WgradProblem(C.Structure):
     _fields_ = [("dy", c_vp), ("x", c_vp), ("dw", c_vp), ("N", c_i64), ("K", c_i64), ("ldy", c_i64), ("ldx", c_i64)]
 
 
+class Fp8wEntry(C.Structure):
+    _fields_ = [("w", c_vp), ("q", c_vp), ("sq", c_vp), ("qt", c_vp), ("sqt", c_vp),
+                ("rows", c_i32), ("cols", c_i32), ("ld", c_i32), ("ldqt", c_i32),
+                ("row_begin", c_i64), ("unit_begin", c_i64), ("part_begin", c_i64)]
+
+
 class ImageSrc(C.Structure):
     _fields_ = [("src", c_vp), ("H", c_i32), ("W", c_i32), ("row_stride", c_i64)]
 
@@ -138,6 +144,8 @@ _SIGS = {
     "maeclip_gemm_fp8": (c_i32, [C.POINTER(GemmArgs), c_vp, c_vp, c_vp]),
     "maeclip_quant_rows_fp8": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "maeclip_quant_cols_fp8_workspace": (c_i64, [c_i64, c_i64]),
+    "maeclip_quant_weights_fp8_prepare": (c_i64, [C.POINTER(Fp8wEntry), c_i32]),
+    "maeclip_quant_weights_fp8": (c_i32, [c_vp, C.POINTER(Fp8wEntry), c_i32, c_vp, c_i64, c_vp]),
     "maeclip_quant_cols_fp8": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "maeclip_wgrad_grouped_workspace": (c_i64, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32]),
     "maeclip_wgrad_grouped": (c_i32, [C.POINTER(WgradProblem), c_i32, c_i64, c_i32, c_f32, c_vp, c_i64, c_vp]),

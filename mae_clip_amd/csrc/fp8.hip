@@ -189,7 +189,161 @@ __global__ void __launch_bounds__(256) quant_cols_kernel(const float* __restrict
   }
 }
 
+// ---- all stack weights of a step in three launches (maeclip_quant_weights_fp8)
+// entry lookup: the last entry whose prefix start is <= u (n <= a few hundred)
+__device__ __forceinline__ int wentry(const maeclip_fp8w_entry* __restrict__ e, int n, int64_t u, bool strips) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((strips ? e[mid].unit_begin : e[mid].row_begin) <= u) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// W rows (per output channel): one wave per row of the concatenated row space
+__global__ void __launch_bounds__(256) wq_rows_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                                      int64_t total_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grow = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (grow >= total_rows) return;
+  const maeclip_fp8w_entry& w = e[wentry(e, n, grow, false)];
+  const int64_t r = grow - w.row_begin;
+  const float* xr = w.w + r * w.ld;
+  const int cols = w.cols;
+  float amax = 0.f;
+  for (int c = lane * 8; c < cols; c += 512) {
+    float v[8];
+    Row8<float>::load(xr + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  const float s = amax > 0.f ? amax / E4M3_MAX : 1.f;
+  const float inv = 1.f / s;
+  if (lane == 0) w.sq[r] = s;
+  uint8_t* qr = (uint8_t*)w.q + r * cols;
+  for (int c = lane * 8; c < cols; c += 512) {
+    float v[8];
+    Row8<float>::load(xr + c, v);
+    v2u o;
+    o[0] = cvt4<false>(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+    o[1] = cvt4<false>(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
+    *(v2u*)(qr + c) = o;
+  }
+}
+
+// W^T: units = (entry, 64-column strip, 256-row chunk), chunk fastest
+__global__ void __launch_bounds__(256) wq_cols_amax_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int64_t gu = blockIdx.x;
+  const maeclip_fp8w_entry& w = e[wentry(e, n, gu, true)];
+  const int lu = (int)(gu - w.unit_begin), nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+  const int c0 = (lu / nch) * 64, r0 = (lu % nch) * QC_ROWS;
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6, col = c0 + tc;
+  float amax = 0.f;
+  if (col < w.cols)
+    for (int r = r0 + tr; r < min(w.rows, r0 + QC_ROWS); r += 4) amax = fmaxf(amax, fabsf(w.w[(int64_t)r * w.ld + col]));
+  red[tr][tc] = amax;
+  __syncthreads();
+  if (tr == 0 && col < w.cols)
+    part[w.part_begin + (int64_t)(lu % nch) * w.cols + col] =
+        fmaxf(fmaxf(red[0][tc], red[1][tc]), fmaxf(red[2][tc], red[3][tc]));
+}
+
+__global__ void __launch_bounds__(256) wq_cols_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                                      const float* __restrict__ part) {
+  __shared__ float tile[64][65];
+  __shared__ float inv_s[64];
+  const int64_t gu = blockIdx.x;
+  const maeclip_fp8w_entry& w = e[wentry(e, n, gu, true)];
+  const int lu = (int)(gu - w.unit_begin), nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+  const int c0 = (lu / nch) * 64, r0 = (lu % nch) * QC_ROWS;
+  const int rows = w.rows, cols = w.cols;
+  if (threadIdx.x < 64) {
+    const int col = c0 + threadIdx.x;
+    float a = 0.f;
+    if (col < cols)
+      for (int k = 0; k < nch; ++k) a = fmaxf(a, part[w.part_begin + (int64_t)k * cols + col]);
+    const float s = a > 0.f ? a / E4M3_MAX : 1.f;
+    inv_s[threadIdx.x] = 1.f / s;
+    if (r0 == 0 && col < cols) w.sqt[col] = s;
+  }
+  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6, col = c0 + tc;
+  uint8_t* qt = (uint8_t*)w.qt;
+  for (int rb = r0; rb < min(rows, r0 + QC_ROWS); rb += 64) {
+    __syncthreads();
+    for (int rr = tr; rr < 64; rr += 4) {
+      const int r = rb + rr;
+      tile[rr][tc] = (r < rows && col < cols) ? w.w[(int64_t)r * w.ld + col] : 0.f;
+    }
+    __syncthreads();
+    const int tc2 = threadIdx.x >> 2, seg = threadIdx.x & 3;
+    const float inv = inv_s[tc2];
+    if (c0 + tc2 < cols && rb + seg * 16 < rows) {
+      uint8_t* dst = qt + (int64_t)(c0 + tc2) * w.ldqt + rb + seg * 16;
+      v4u o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rr = seg * 16 + 4 * k;
+        o[k] = cvt4<false>(tile[rr][tc2] * inv, tile[rr + 1][tc2] * inv, tile[rr + 2][tc2] * inv,
+                           tile[rr + 3][tc2] * inv);
+      }
+      if (rb + seg * 16 + 16 <= rows) {
+        *(v4u*)dst = o;
+      } else {
+        for (int k = 0; k < 16 && rb + seg * 16 + k < rows; ++k) dst[k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// host side of the batched weight quantisation: prefix sums filled here
+extern "C" int64_t maeclip_quant_weights_fp8_prepare(maeclip_fp8w_entry* host, int32_t n) {
+  int64_t rows = 0, units = 0, part = 0;
+  for (int i = 0; i < n; ++i) {
+    maeclip_fp8w_entry& w = host[i];
+    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+    w.row_begin = rows;
+    w.unit_begin = units;
+    w.part_begin = part;
+    rows += w.rows;
+    units += (int64_t)((w.cols + 63) / 64) * nch;
+    part += (int64_t)nch * w.cols;
+  }
+  return part * 4;   // workspace bytes (column partial maxima)
+}
+
+extern "C" int32_t maeclip_quant_weights_fp8(const maeclip_fp8w_entry* dev, const maeclip_fp8w_entry* host, int32_t n,
+                                             float* workspace, int64_t ws_bytes, void* stream) {
+  MC_CHECK_ARG(dev && host && n > 0, "maeclip_quant_weights_fp8: bad arguments");
+  int64_t rows = 0, units = 0, part = 0;
+  for (int i = 0; i < n; ++i) {
+    const maeclip_fp8w_entry& w = host[i];
+    MC_CHECK_ARG(w.w && w.q && w.sq && w.qt && w.sqt && w.rows > 0 && w.cols > 0 && w.cols % 8 == 0 &&
+                     w.ld >= w.cols && w.ld % 8 == 0 && w.ldqt >= w.rows && w.ldqt % 16 == 0,
+                 "maeclip_quant_weights_fp8: bad entry %d", i);
+    MC_CHECK_ARG(w.row_begin == rows && w.unit_begin == units && w.part_begin == part,
+                 "maeclip_quant_weights_fp8: entries not prepared (maeclip_quant_weights_fp8_prepare)");
+    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+    rows += w.rows;
+    units += (int64_t)((w.cols + 63) / 64) * nch;
+    part += (int64_t)nch * w.cols;
+  }
+  MC_CHECK_ARG(workspace && ws_bytes >= part * 4, "maeclip_quant_weights_fp8: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wq_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, dev, n, rows);
+  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(rows)");
+  hipLaunchKernelGGL(wq_cols_amax_kernel, dim3((unsigned)units), dim3(256), 0, s, dev, n, workspace);
+  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(cols amax)");
+  hipLaunchKernelGGL(wq_cols_kernel, dim3((unsigned)units), dim3(256), 0, s, dev, n, (const float*)workspace);
+  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(cols)");
+  return 0;
+}
 
 extern "C" int32_t maeclip_quant_rows_fp8(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ld,
                                           void* q, int64_t ldq, float* scales, int32_t fmt, void* stream) {

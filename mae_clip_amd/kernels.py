@@ -132,6 +132,37 @@ def quant_cols_fp8(w, out=None):
     return out
 
 
+class Fp8WeightPlan:
+    """fp8 operands of a set of fp32 GEMM weights W [N, K], refreshed for all of
+    them in one maeclip_quant_weights_fp8 call (three launches): W per output
+    channel (forward B operand) and W^T per input channel (dgrad B operand)."""
+
+    def __init__(self, weights, device):
+        n = len(weights)
+        self.ops = []
+        self.host = (L.Fp8wEntry * n)()
+        for i, w in enumerate(weights):
+            N, Kd = w.shape
+            ldqt = (N + 15) // 16 * 16
+            wq = Fp8Rows(torch.empty((N, Kd), device=device, dtype=torch.uint8),
+                         torch.empty((N,), device=device, dtype=torch.float32), FP8_E4M3)
+            wt = Fp8Rows(torch.empty((Kd, ldqt), device=device, dtype=torch.uint8)[:, :N],
+                         torch.empty((Kd,), device=device, dtype=torch.float32), FP8_E4M3)
+            self.ops.append((wq, wt))
+            e = self.host[i]
+            e.w, e.q, e.sq, e.qt, e.sqt = w.data_ptr(), wq.q.data_ptr(), wq.s.data_ptr(), wt.q.data_ptr(), wt.s.data_ptr()
+            e.rows, e.cols, e.ld, e.ldqt = N, Kd, w.stride(0), ldqt
+        nb = int(L.lib().maeclip_quant_weights_fp8_prepare(self.host, n))
+        self.ws_bytes = max(nb, 4)
+        self.ws = torch.empty((self.ws_bytes // 4,), device=device, dtype=torch.float32)
+        self.dev = torch.frombuffer(bytearray(bytes(self.host)), dtype=torch.uint8).to(device)
+        self.n = n
+
+    def run(self):
+        _call("maeclip_quant_weights_fp8", self.dev.data_ptr(), self.host, self.n, self.ws.data_ptr(), self.ws_bytes,
+              _stream())
+
+
 def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=None, aux=None, aux_out=None,
              resid=None, colsum=None):
     """Cout[M, N] = epilogue(alpha * (s_A[m] s_B[n]) * sum_k qA[m, k] qB[n, k]) on the

@@ -71,11 +71,26 @@ class WeightCache:
         self.buf = None
         self.fp8 = fp8
         self.f8 = {}
+        self.f8_params = []   # fp32 masters quantised by refresh() in fp8 mode
+        self.f8_plan = None
+        self.f8_key = None
 
     def register(self, p: torch.Tensor, shape2d):
         self.entries.append((p, tuple(shape2d)))
 
+    def register_fp8(self, p: torch.Tensor):
+        """p [N, K]: an fp8 stack GEMM weight (used in fp8 mode only)."""
+        self.f8_params.append(p)
+
     def refresh(self, dtype):
+        if self.fp8 and dtype == torch.bfloat16 and self.f8_params:
+            # all fp8 weight operands of the step: one batched quantisation
+            key = tuple(p.data_ptr() for p in self.f8_params)
+            if key != self.f8_key:
+                self.f8_plan = K.Fp8WeightPlan([p.detach() for p in self.f8_params], self.f8_params[0].device)
+                self.f8 = {id(p): ops for p, ops in zip(self.f8_params, self.f8_plan.ops)}
+                self.f8_key = key
+            self.f8_plan.run()
         if dtype == torch.float32 or not self.entries:
             return
         key = tuple(p.data_ptr() for p, _ in self.entries)
@@ -100,15 +115,13 @@ class WeightCache:
         return self.views[id(p)]
 
     def get_fp8(self, p: torch.Tensor):
-        """(W, W^T) fp8 operands of GEMM weight p [N, K], quantised now (call
-        once per forward: the quantisation is part of the captured step)."""
+        """(W, W^T) fp8 operands of GEMM weight p [N, K] for this step: the
+        ones refresh() quantised (registered weights), else quantised now."""
+        if self.f8_plan is not None and id(p) in self.f8:
+            return self.f8[id(p)]
         w = p.detach()
-        prev = self.f8.get(id(p))
-        if prev is not None and prev[0].q.device != w.device:
-            prev = None
-        wq = K.quant_rows_fp8(w, K.FP8_E4M3, out=prev[0] if prev else None)
-        wt = K.quant_cols_fp8(w, out=prev[1] if prev else None)
-        self.f8[id(p)] = (wq, wt)
+        wq = K.quant_rows_fp8(w, K.FP8_E4M3)
+        wt = K.quant_cols_fp8(w)
         return wq, wt
 
 
@@ -220,6 +233,7 @@ class VisionTransformer(nn.Module):
         for blk in self.blocks:
             for p in blk.gemm_weights():
                 cache.register(p, p.shape)
+                cache.register_fp8(p)
 
     def forward_tokens(self, img, dtype, cache, ids_shuffle=None, ids_restore=None, keep=None, world=1):
         _require_device(img, "image batch")

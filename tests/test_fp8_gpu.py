@@ -136,3 +136,19 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
             worst = max(worst, (g8[n] - gbn).norm().item() / den)
     print(f"worst relative L2 gradient deviation fp8 vs bf16: {worst:.4f}")
     assert worst < 0.15, worst
+
+
+def test_batched_weight_quantisation_matches_single(dev):
+    """maeclip_quant_weights_fp8 (all stack weights in three launches) ==
+    the per-weight quant_rows_fp8 / quant_cols_fp8, bit for bit, over weights of
+    different shapes (row counts not multiples of 64 / 256)."""
+    g = torch.Generator().manual_seed(3)
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096), (200, 136), (72, 512)]
+    ws = [(torch.randn(s, generator=g) * torch.logspace(-2, 1, s[1])).to(dev) for s in shapes]
+    plan = K.Fp8WeightPlan(ws, dev)
+    plan.run()
+    for w, (wq, wt) in zip(ws, plan.ops):
+        r = K.quant_rows_fp8(w, K.FP8_E4M3)
+        c = K.quant_cols_fp8(w)
+        assert torch.equal(wq.q, r.q) and torch.equal(wq.s, r.s)
+        assert torch.equal(wt.q, c.q) and torch.equal(wt.s, c.s)
