@@ -44,6 +44,16 @@ bool getenv_flag(const char* name) {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
 
+#ifdef ATTN_STAMPS
+// diagnostic build only: s_memtime per wave of the first 4096 backward
+// workgroups at start / prologue done / phase 1 done / phase 2 start / phase 2
+// done / exit
+__device__ uint64_t g_attn_stamps[4096 * MAXW * 8];
+#define ASTAMP(k) do { if (lane == 0 && blockIdx.x < 4096) g_attn_stamps[((int64_t)blockIdx.x * MAXW + wave) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define ASTAMP(k) do {} while (0)
+#endif
+
 template <typename T, int HD> struct Img {
   static constexpr bool BF = sizeof(T) == 2;
   static constexpr int ROWB = BF ? HD * 2 : HD * 4 + 16;
@@ -409,6 +419,7 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const int npad = (n + 31) & ~31;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  ASTAMP(0);
   // bf16: Q, K, V, dO images resident together. fp32 parity mode (rows twice
   // as wide) holds two at a time so that n = 197 at HD = 64 fits: phase 1
   // keeps Q, dO in LDS and reads each wave's K/V tile from HBM, phase 2
@@ -441,6 +452,19 @@ attn_bwd_kernel(const maeclip_attn_args a) {
     for (int i = threadIdx.x; i < nv; i += NTH) tail[i] = v4u{0u, 0u, 0u, 0u};
   }
   __syncthreads();
+  ASTAMP(1);
+  if (a.colsum_partial && threadIdx.x < NW * HD) {
+    // v-bias gradient: sum over keys of dV = sum over queries of dO (softmax
+    // rows sum to 1; the backward runs without attention dropout). Row group
+    // r0 of column d -> cs[r0][2 HD + d]; the k-bias gradient is identically
+    // zero (softmax is invariant to a per-query constant) and stays 0.
+    constexpr int EPC = 16 / (int)sizeof(T);
+    const int d = threadIdx.x % HD, r0 = threadIdx.x / HD;
+    float sv = 0.f;
+    for (int r = r0; r < n; r += NW)
+      sv += ld_as_f<T>((const T*)(Di + I::chunk(r, d / EPC) + (d % EPC) * (int)sizeof(T)));
+    cs[r0 * 3 * HD + 2 * HD + d] = sv;
+  }
 
   const float c = a.scale * LOG2E;
   T* dqkv = (T*)a.dqkv + (int64_t)b * n * a.ld_dqkv;
@@ -513,25 +537,9 @@ attn_bwd_kernel(const maeclip_attn_args a) {
         st4<T>(rowp + 2 * HH + 16 * dt + 4 * g, dv[dt]);
       }
     }
-    if (a.colsum_partial) {
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float sk = kok ? dk[dt][i] * a.scale : 0.f, sv = kok ? dv[dt][i] : 0.f;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            sk += __shfl_xor(sk, o, 64);
-            sv += __shfl_xor(sv, o, 64);
-          }
-          if ((lane & 15) == 0) {
-            cs[wave * 3 * HD + HD + 16 * dt + 4 * g + i] += sk;
-            cs[wave * 3 * HD + 2 * HD + 16 * dt + 4 * g + i] += sv;
-          }
-        }
-    }
   }
 
+  ASTAMP(2);
   if (TWO) {
     // phase-1 reads of the Q / dO images are done: K, V take their slots
     __syncthreads();
@@ -542,6 +550,12 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   }
   // ---------------- phase 2: dQ (wave owns 16-query tiles)
   if (SDS) __syncthreads();   // every wave's dS columns are in LDS
+  ASTAMP(3);
+  float cq[HD / 16][4];  // per-lane running sum of this wave's dQ rows (q-bias gradient)
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cq[dt][i] = 0.f;
   for (int qt = wave; qt < nkt; qt += NW) {
     const int q0 = qt * 16;
     const int q = q0 + (lane & 15);
@@ -600,19 +614,24 @@ attn_bwd_kernel(const maeclip_attn_args a) {
       T* rowp = dqkv + (int64_t)q * a.ld_dqkv + h * HD;
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) st4<T>(rowp + 16 * dt + 4 * g, dq[dt] * a.scale);
-    }
-    if (a.colsum_partial) {
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float sq = qok ? dq[dt][i] * a.scale : 0.f;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) sq += __shfl_xor(sq, o, 64);
-          if ((lane & 15) == 0) cs[wave * 3 * HD + 16 * dt + 4 * g + i] += sq;
-        }
+        for (int i = 0; i < 4; ++i) cq[dt][i] += dq[dt][i];
     }
   }
+  if (a.colsum_partial) {
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sq = cq[dt][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) sq += __shfl_xor(sq, o, 64);
+        if ((lane & 15) == 0) cs[wave * 3 * HD + 16 * dt + 4 * g + i] = sq * a.scale;
+      }
+  }
+  ASTAMP(4);
   if (a.colsum_partial) {
     __syncthreads();
     // colsum_partial row b: [3*H*HD], this head's q/k/v column slices
@@ -624,6 +643,7 @@ attn_bwd_kernel(const maeclip_attn_args a) {
       a.colsum_partial[(int64_t)b * 3 * HH + part * HH + h * HD + d] = s;
     }
   }
+  ASTAMP(5);
 }
 
 template <typename T, int HD> size_t fwd_lds(int n) {
@@ -741,6 +761,12 @@ int dispatch(const maeclip_attn_args* a, bool bwd, void* stream) {
 }
 
 }  // namespace
+
+#ifdef ATTN_STAMPS
+extern "C" int maeclip_debug_attn_stamps(uint64_t* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), sizeof(uint64_t) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int32_t maeclip_attn_fwd(const maeclip_attn_args* a, void* stream) { return dispatch(a, false, stream); }
 extern "C" int32_t maeclip_attn_bwd(const maeclip_attn_args* a, void* stream) { return dispatch(a, true, stream); }

@@ -27,6 +27,7 @@
 // barrier-delimited segment one group issues its ds_reads/DMA while the other
 // group's 16 MFMAs run (one wave of each group per SIMD).
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/maeclip.h"
 
 namespace {
@@ -37,6 +38,10 @@ enum { EPI_NONE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_DGELU = 3, EPI_GELU_D = 4,
 typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ int swz_rc(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
+
+#ifndef GEMM4_EPI_PF
+#define GEMM4_EPI_PF 2
+#endif
 
 #ifdef GEMM4_STAMPS
 __device__ uint64_t g_stamps[256 * 8 * 2 * 4];
@@ -202,6 +207,22 @@ __device__ __forceinline__ void epilogue4_slab(float* __restrict__ slab, int M, 
   }
 }
 
+// whole 256x256 fp32 tile (stream-K partial) into a dense slot [256][256]
+__device__ __forceinline__ void epilogue4_tile(float* __restrict__ t, v4f (&acc)[8][4], int wm, int wn, int lane) {
+  const int g = lane >> 4;
+  swap_pairs(acc);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ml = 128 * wm + 64 * (i >> 2) + 16 * (i & 3) + (lane & 15);
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      float* d = t + ml * 256 + 64 * wn + 32 * ni + 16 * (g & 1) + 8 * (g >> 1);
+      *(v4f*)d = acc[i][2 * ni];
+      *(v4f*)(d + 4) = acc[i][2 * ni + 1];
+    }
+  }
+}
+
 // sa / sb (fp8 only): per-row dequantisation scale of A [M] and per-column
 // scale of B [N]; the product scales the accumulator before alpha / bias.
 template <typename OutT, int EPI, bool F8 = false>
@@ -226,9 +247,13 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
     bias8[ni][0] = args.bias ? *(const v4f*)(args.bias + n) : v4f{0.f, 0.f, 0.f, 0.f};
     bias8[ni][1] = args.bias ? *(const v4f*)(args.bias + n + 4) : v4f{0.f, 0.f, 0.f, 0.f};
   }
-  // chunk c = row fragment i = c (hh = c >> 2); q = ni
-  v4u ax[2][2];
-  v4f rs[2][2][2];
+  // chunk c = row fragment i = c (hh = c >> 2); q = ni. The aux / residual
+  // reads of chunk c + PF - 1 are issued before chunk c is finished: PF - 1
+  // HBM round trips in flight instead of one (the main-loop operand registers
+  // are dead here, so the ring fits the 256-register budget).
+  constexpr int PF = GEMM4_EPI_PF;
+  v4u ax[PF][2];
+  v4f rs[PF][2][2];
   auto load_chunk = [&](int c, int buf) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -248,10 +273,13 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
   for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
     for (int r = 0; r < 8; ++r) csum[ni][r] = 0.f;
-  if (LOAD_AUX || LOAD_RES) load_chunk(0, 0);
+  if (LOAD_AUX || LOAD_RES) {
+#pragma unroll
+    for (int c = 0; c < PF - 1; ++c) load_chunk(c, c);
+  }
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    if ((LOAD_AUX || LOAD_RES) && c + 1 < 8) load_chunk(c + 1, (c + 1) & 1);
+    if ((LOAD_AUX || LOAD_RES) && c + PF - 1 < 8) load_chunk(c + PF - 1, (c + PF - 1) % PF);
     __builtin_amdgcn_sched_barrier(0);   // keep chunk c+1's loads ahead of chunk c's stores
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -292,7 +320,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
         }
       }
       if (LOAD_AUX) {
-        const v4u pk = ax[c & 1][q];
+        const v4u pk = ax[c % PF][q];
         if (EPI == EPI_MUL_AUX) {
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
@@ -312,8 +340,8 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
         }
       }
       if (LOAD_RES && has_res) {
-        lo += rs[c & 1][q][0];
-        hi += rs[c & 1][q][1];
+        lo += rs[c % PF][q][0];
+        hi += rs[c % PF][q][1];
       }
       if (m < M && n < N) {
         OutT* cp = C + (int64_t)m * args.ldc + n;
@@ -382,6 +410,7 @@ struct Unit4 {
   int m0, n0;
   int kbeg, nt;       // first k and number of 64-wide K-tiles of this unit
   int slice, prob;
+  int slot;           // stream-K partial tile: workspace slot; -1 = final result
 };
 
 // Grouped weight gradients (maeclip_wgrad_grouped): dW_p[N_p, K_p] (+)=
@@ -400,6 +429,11 @@ struct WgProb {
 };
 struct WgGroup {
   int np, S, T, Mtok;
+  // stream-K remainder (skw > 0): tiles [0, Tdp) run whole (Tdp a multiple of
+  // the grid), the K-tiles of tiles [Tdp, T) are dealt out evenly, skw per
+  // block in block-position order; a tile cut between blocks leaves fp32
+  // partials in 256x256 slots (2 per block) summed by wgrad4_sk_reduce_kernel
+  int Tdp, skw, NT;
   float beta;
   float* ws;
   WgProb p[WG_MAX];
@@ -425,7 +459,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   // grouped = slice-major (slice, tile) pairs, so neighbouring units share operands
   int T, gn = 1, klen = 0;
   if (GRP) {
-    T = gp->T * gp->S;
+    T = gp->skw > 0 ? gp->Tdp : gp->T * gp->S;
     klen = ((gp->Mtok + gp->S - 1) / gp->S + KT - 1) / KT * KT;
   } else {
     const int gm = ((int)args.M + 255) / 256;
@@ -469,6 +503,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     w.kbeg = w.slice * klen;
     const int kend = min(w.K, w.kbeg + klen);
     w.nt = kend > w.kbeg ? (kend - w.kbeg) / KT : 0;
+    w.slot = -1;
     return w;
   };
 
@@ -481,6 +516,30 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   const int cq = T / 8, cr = T % 8;
   const int cbeg = x8 < cr ? x8 * (cq + 1) : cr * (cq + 1) + (x8 - cr) * cq;
   const int cend = cbeg + cq + (x8 < cr ? 1 : 0);
+  // this block's jobs: its whole tiles, then (grouped stream-K) its K range of
+  // the remainder tiles
+  const int ndp = cbeg + li < cend ? (cend - (cbeg + li) + nbx - 1) / nbx : 0;
+  int ska = 0, skb = 0, nsk = 0, skp = 0;
+  if (GRP && gp->skw > 0) {
+    skp = G % 8 == 0 ? x8 * (G / 8) + li : (int)blockIdx.x;   // XCD-contiguous positions
+    const int tot = (gp->T - gp->Tdp) * gp->NT;
+    ska = min(skp * gp->skw, tot);
+    skb = min(ska + gp->skw, tot);
+    nsk = skb > ska ? (skb - 1) / gp->NT - ska / gp->NT + 1 : 0;
+  }
+  auto job = [&](int j) -> Unit4 {
+    if (j < ndp) return unit(cbeg + li + j * nbx);
+    const int s = j - ndp, NT = gp->NT;
+    const int tl = ska / NT + s;
+    const int k0 = s == 0 ? ska % NT : 0;
+    const int k1 = tl == (skb - 1) / NT ? (skb - 1) % NT + 1 : NT;
+    Unit4 w = unit(gp->Tdp + tl);
+    w.kbeg = k0 * KT;
+    w.nt = k1 - k0;
+    w.slot = (k0 == 0 && k1 == NT) ? -1 : 2 * skp + (s == 0 ? 0 : 1);
+    return w;
+  };
+  const int njobs = ndp + nsk;
 
   // per-lane DMA byte offsets of a unit's operands (loop invariants of its K loop)
   auto offsets = [&](const Unit4& w, int (&vA)[2][2], int (&vB)[2][2]) {
@@ -533,11 +592,10 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 #else
 #define STAMP(k) do {} while (0)
 #endif
-  for (int tile = cbeg + li; tile < cend; tile += nbx) {
+  for (int jb = 0; jb < njobs; ++jb) {
     STAMP(0);
-    const Unit4 u = unit(tile);
+    const Unit4 u = job(jb);
     const int m0 = u.m0, n0 = u.n0, nt = u.nt;
-    const int tnext = tile + nbx;
     int voA[2][2], voB[2][2];
     offsets(u, voA, voB);
     if (nt > 0 && !primed) prologue(u);
@@ -623,8 +681,8 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (!more1 && tnext < cend) {
-          const Unit4 un = unit(tnext);
+        if (!more1 && jb + 1 < njobs) {
+          const Unit4 un = job(jb + 1);
           if (un.nt > 0) {
             prologue(un);
             primed = true;
@@ -641,7 +699,9 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     STAMP(2);
     if (GRP) {
       const WgProb& q = gp->p[u.prob];
-      if (SPLIT) {
+      if (u.slot >= 0) {
+        epilogue4_tile(gp->ws + (int64_t)u.slot * 65536, acc, wm, wn, lane);
+      } else if (SPLIT) {
         epilogue4_slab(gp->ws + q.slab_off + (int64_t)u.slice * q.N * q.K, q.N, q.K, 1.f, acc, m0, n0, wm, wn, lane);
       } else {
         maeclip_gemm_args ea = args;
@@ -699,6 +759,32 @@ __global__ void __launch_bounds__(256) wgrad4_reduce_kernel(const WgGroup grp) {
     v4f v = *(const v4f*)(ws + e);
     for (int s = 1; s < grp.S; ++s) v += *(const v4f*)(ws + s * NK + e);
     float* d = q.dw + e;
+    if (grp.beta != 0.f) v += grp.beta * *(const v4f*)d;
+    *(v4f*)d = v;
+  }
+}
+
+// stream-K remainder tile blockIdx.x: the partial slots of the blocks that
+// shared its K range, in block-position order (fixed summation order), + beta dW
+__global__ void __launch_bounds__(256) wgrad4_sk_reduce_kernel(const WgGroup grp) {
+  const int r = blockIdx.x, NT = grp.NT, w = grp.skw;
+  const int p0 = r * NT / w, p1 = ((r + 1) * NT - 1) / w;
+  if (p0 == p1) return;   // one block ran the whole tile and wrote dW itself
+  const int tile = grp.Tdp + r;
+  int p = 0;
+  while (p + 1 < grp.np && grp.p[p + 1].tile_begin <= tile) ++p;
+  const WgProb& q = grp.p[p];
+  const int local = tile - q.tile_begin, gnp = (q.K + 255) / 256;
+  const int m0 = (local / gnp) * 256, n0 = (local % gnp) * 256;
+  for (int e = threadIdx.x * 4; e < 65536; e += 1024) {
+    const int m = m0 + (e >> 8), n = n0 + (e & 255);
+    if (m >= q.N || n >= q.K) continue;   // K % 8 == 0: a 4-group is all in or all out
+    v4f v = {0.f, 0.f, 0.f, 0.f};
+    for (int c = p0; c <= p1; ++c) {
+      const int slot = 2 * c + ((c * w) / NT == r ? 0 : 1);
+      v += *(const v4f*)(grp.ws + (int64_t)slot * 65536 + e);
+    }
+    float* d = q.dw + (int64_t)m * q.K + n;
     if (grp.beta != 0.f) v += grp.beta * *(const v4f*)d;
     *(v4f*)d = v;
   }
@@ -898,6 +984,20 @@ int wg_splits(int T, int64_t M) {
   return best;
 }
 
+// Stream-K remainder: K-tiles per block when the T tiles leave a partial last
+// wave on the grid (0 = none). Each block then runs floor(T / ncu) whole tiles
+// plus skw K-tiles of the remainder, so every block does the same work; a
+// block's range cuts at most two tiles (two 256 KB fp32 slots). Below 8
+// K-tiles per block the slot write + reduce outweighs the balance.
+int wg_skw(int T, int64_t M) {
+  const char* e = getenv("MAECLIP_WG_SK");   // 0: uniform split-K slices instead (A/B)
+  const bool enabled = !(e && *e == '0');
+  const int G = wg_ncu(), R = T % G;
+  if (R == 0 || !enabled) return 0;
+  const int64_t skw = ((int64_t)R * (M / 64) + G - 1) / G;
+  return skw >= 8 ? (int)skw : 0;
+}
+
 int64_t wg_chunk_ws(const maeclip_wgrad_problem* pr, int n, int64_t M) {
   int T = 0;
   int64_t nk = 0;
@@ -905,6 +1005,7 @@ int64_t wg_chunk_ws(const maeclip_wgrad_problem* pr, int n, int64_t M) {
     T += wg_tiles(pr[i]);
     nk += pr[i].N * pr[i].K;
   }
+  if (wg_skw(T, M) > 0) return (int64_t)2 * wg_ncu() * 65536 * 4;
   const int S = wg_splits(T, M);
   return S > 1 ? (int64_t)S * nk * 4 : 0;
 }
@@ -978,6 +1079,18 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       T += wg_tiles(q);
     }
     g.T = T;
+    g.skw = wg_skw(T, M);
+    if (g.skw > 0) {
+      g.S = 1;
+      g.NT = (int)(M / 64);
+      g.Tdp = T - T % wg_ncu();
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(wg_ncu()), dim3(512), LDS_BYTES, s, g);
+      MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k)");
+      hipLaunchKernelGGL(wgrad4_sk_reduce_kernel, dim3(T - g.Tdp), dim3(256), 0, s, g);
+      MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k reduce)");
+      continue;
+    }
     g.S = wg_splits(T, M);
     if (g.S > 1) {
       for (int i = 0; i < n; ++i) {

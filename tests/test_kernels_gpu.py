@@ -131,7 +131,13 @@ def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     tolb = 1e-4 if dtype == torch.float32 else 3e-2
     assert (dqkv.double() - g).abs().max().item() / gs < tolb
     cs = part.sum(0)
-    assert (cs.double() - g.view(B, n, -1).sum(1).sum(0)).abs().max().item() / (gs * n) < tolb
+    gsum = g.view(B * n, 3, H * hd).sum(0)
+    assert (cs.double() - gsum.view(-1)).abs().max().item() / (gs * n) < tolb
+    # the identities the bias partials use: sum over keys of dK is zero (softmax
+    # is invariant to a per-query constant), sum over keys of dV = sum of dO
+    assert gsum[1].abs().max().item() < 1e-9 * gs * n
+    assert (cs.view(3, -1)[1] == 0).all()
+    assert (cs.view(3, -1)[2].double() - dout.double().sum(0)).abs().max().item() < 1e-4 * max(1.0, n ** 0.5)
 
 
 def test_attention_key_mask(dev):
@@ -350,18 +356,27 @@ def test_wgrad_splitk_v4(dev, mnk):
     assert torch.equal(dW, dW2)
 
 
-@pytest.mark.parametrize("case", ["encoder4", "decoder2x4", "few_tiles_splitk", "strided", "fp32_fallback"])
-def test_wgrad_grouped(dev, case):
+@pytest.mark.parametrize("case", ["encoder4", "decoder2x4", "few_tiles_splitk", "strided", "fp32_fallback",
+                                  "whole_plus_streamk", "uniform_slices"])
+def test_wgrad_grouped(dev, case, monkeypatch):
     """maeclip_wgrad_grouped: the 4 weight gradients of transformer blocks
-    (qkv, proj, fc1, fc2) in one launch vs fp64 torch; S = 1 and split-K
-    groups, strided dy (a column slice), beta accumulation, the per-problem
-    fallback for fp32 -- bit-identical across repeated runs (deterministic)."""
+    (qkv, proj, fc1, fc2) in one launch vs fp64 torch; stream-K remainder
+    (fewer tiles than CUs; whole tiles + a remainder dealt out by K-tiles, with
+    edge tiles in both parts), uniform split-K slices (MAECLIP_WG_SK=0, and too
+    little K for stream-K), strided dy (a column slice), beta accumulation, the
+    per-problem fallback for fp32 -- bit-identical across repeated runs."""
     from mae_clip_amd import _lib
     dt = torch.float32 if case == "fp32_fallback" else torch.bfloat16
     if case in ("encoder4", "strided", "fp32_fallback"):
         M, shapes = 3200, [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
-    elif case == "decoder2x4":
+    elif case in ("decoder2x4", "uniform_slices"):
         M, shapes = 6400, [(1536, 512), (512, 512), (2048, 512), (512, 2048)] * 2
+        if case == "uniform_slices":
+            monkeypatch.setenv("MAECLIP_WG_SK", "0")
+    elif case == "whole_plus_streamk":
+        # 144 + 108 + 132 = 384 tiles: 256 whole, 128 (2600-row edge tiles among
+        # them) over the grid by K-tiles
+        M, shapes = 2048, [(3072, 3072), (3072, 2056), (2600, 3072)]
     else:
         M, shapes = 4096, [(512, 256), (256, 512)]   # 4 tiles -> split-K slices
     items, refs = [], []
