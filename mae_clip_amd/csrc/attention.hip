@@ -266,7 +266,8 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int bid = xcd_chunk_id(blockIdx.x, gridDim.x);
+  const int b = bid / H, h = bid % H;
   const int npad = (n + 63) & ~63;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   char* Kimg = smem;
@@ -416,7 +417,8 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int bid = xcd_chunk_id(blockIdx.x, gridDim.x);
+  const int b = bid / H, h = bid % H;
   const int npad = (n + 31) & ~31;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   ASTAMP(0);

@@ -52,6 +52,15 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 // ------------------------------------------------------------- device helpers
+// XCD-chunked workgroup id. The dispatcher deals consecutive workgroups
+// round-robin over the 8 XCDs; this bijective remap hands each XCD a contiguous
+// range of logical ids, so workgroups that read the same rows (e.g. the heads
+// of one sample) share that XCD's L2 (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_chunk_id(int bid, int G) {
+  const int q = G >> 3, r = G & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
 __device__ __forceinline__ float bf2f(bf16_t u) {
   return __uint_as_float(((unsigned)u) << 16);
 }

@@ -764,8 +764,12 @@ __global__ void __launch_bounds__(256) wgrad4_reduce_kernel(const WgGroup grp) {
   }
 }
 
-// stream-K remainder tile blockIdx.x: the partial slots of the blocks that
-// shared its K range, in block-position order (fixed summation order), + beta dW
+// stream-K remainder tile blockIdx.x, element chunk blockIdx.y (of SKR_CHUNKS):
+// the partial slots of the blocks that shared its K range, in block-position
+// order (fixed summation order), + beta dW. Chunking the tile over SKR_CHUNKS
+// workgroups keeps the reduce at HBM rate when only a few tiles are cut (the
+// encoder's 16 remainder tiles each carry ~17 slots).
+constexpr int SKR_CHUNKS = 16;
 __global__ void __launch_bounds__(256) wgrad4_sk_reduce_kernel(const WgGroup grp) {
   const int r = blockIdx.x, NT = grp.NT, w = grp.skw;
   const int p0 = r * NT / w, p1 = ((r + 1) * NT - 1) / w;
@@ -776,7 +780,8 @@ __global__ void __launch_bounds__(256) wgrad4_sk_reduce_kernel(const WgGroup grp
   const WgProb& q = grp.p[p];
   const int local = tile - q.tile_begin, gnp = (q.K + 255) / 256;
   const int m0 = (local / gnp) * 256, n0 = (local % gnp) * 256;
-  for (int e = threadIdx.x * 4; e < 65536; e += 1024) {
+  constexpr int CH = 65536 / SKR_CHUNKS;
+  for (int e = blockIdx.y * CH + threadIdx.x * 4; e < (int)(blockIdx.y + 1) * CH; e += 1024) {
     const int m = m0 + (e >> 8), n = n0 + (e & 255);
     if (m >= q.N || n >= q.K) continue;   // K % 8 == 0: a 4-group is all in or all out
     v4f v = {0.f, 0.f, 0.f, 0.f};
@@ -1087,7 +1092,7 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
       hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(wg_ncu()), dim3(512), LDS_BYTES, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k)");
-      hipLaunchKernelGGL(wgrad4_sk_reduce_kernel, dim3(T - g.Tdp), dim3(256), 0, s, g);
+      hipLaunchKernelGGL(wgrad4_sk_reduce_kernel, dim3(T - g.Tdp, SKR_CHUNKS), dim3(256), 0, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k reduce)");
       continue;
     }
