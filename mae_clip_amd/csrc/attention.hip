@@ -648,6 +648,315 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   ASTAMP(5);
 }
 
+// ======================================================= backward, diagonal
+// bf16, HD = 32, npad <= 256 (the C2/C3 MAE decoder: n = 197): one pass
+// instead of two. Wave w owns key chunk w (32 keys, K/V fragments in
+// registers) and in round r works query chunk c = (w + r) % NC, so in every
+// round each query chunk is touched by exactly one wave. Per (key chunk, query
+// chunk) block it computes S, dP, P, dS once, accumulates dK/dV in registers,
+// transposes dS through a 2 KB per-wave LDS tile (ds_read_b64_tr_b16) and adds
+// dQ^T = K^T dS^T into an fp32 dQ image in LDS (read-modify-write by the one
+// wave that owns the chunk this round; a barrier ends the round). The order
+// in which the waves add to a query chunk is fixed by the schedule, so the
+// result is deterministic, and S / dP / exp are not recomputed for dQ.
+// LDS: Q, dO images, L2 / Dv, dQ f32 [npad][32] (16-B chunks XOR-swizzled by
+// (row >> 1) & 7), NW dS tiles, bias partials: ~78 KB at n = 197 (two
+// workgroups per CU).
+constexpr int DIAG_HD = 32;
+// dQ image: 128-B rows, 16-B chunk ^ (row & 7): conflict-free b128 reads and
+// writes of the (16 rows x 4 chunks) tiles of one MFMA output
+__device__ __forceinline__ int dq_off(int row, int c16) { return row * 128 + ((c16 ^ (row & 7)) << 4); }
+// dS tile [32 keys][32 q] bf16, 64-B rows, 8-B unit ^ F(row) with F linear in
+// row bits 1..3 (found by tools/lds_bank_sim.py): conflict-free for both the
+// ds_write_b64 of the MFMA output (row = key, unit = 4u + g) and the
+// ds_read_b64_tr_b16 of the dQ B operand
+__device__ __forceinline__ int dst_off(int row, int unit) {
+  const int f = ((row >> 1) & 1) ^ (((row >> 2) & 1) << 2) ^ (((row >> 3) & 1) << 1);
+  return row * 64 + ((unit ^ f) << 3);
+}
+// B operand dS^T[key][q] for keys 0..31 (permuted order of pack_p), q = c0 + (lane & 15)
+__device__ __forceinline__ v8s dst_frag(const char* t, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  v8s r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, t + dst_off(16 * h + 4 * g + q, (c0 >> 2) + p)));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * h + e] = x[e];
+  }
+  return r;
+}
+
+// 8 f32 -> the v8s bf16 operand (elements 0-3 from a, 4-7 from b), one
+// v_cvt_pk_bf16_f32 per pair and no lane shuffles
+__device__ __forceinline__ v8s pack8(const v4f& a, const v4f& b) {
+  const v4u u = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(v8s, u);
+}
+
+__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(4)))
+attn_bwd_diag_kernel(const maeclip_attn_args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int HD = DIAG_HD;
+  using I = Img<bf16_t, HD>;
+  const int n = a.n, H = a.H;
+  const int bid = xcd_chunk_id(blockIdx.x, gridDim.x);
+  const int b = bid / H, h = bid % H;
+  const int npad = (n + 31) & ~31, NC = npad >> 5;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4, l15 = lane & 15;
+  const int img = npad * I::ROWB;
+  char* Qi = smem;
+  char* Di = smem + img;
+  float* L2 = (float*)(smem + 2 * img);
+  float* Dv = L2 + npad;
+  char* dQi = (char*)(Dv + npad);                 // f32 [npad][32]
+  char* dst = dQi + npad * 128;                   // NW x [32 keys][32 q] bf16
+  float* cs = (float*)(dst + NW * 2048);          // [2 NW][3 HD] bias partials
+  char* myds = dst + wave * 2048;
+  ASTAMP(0);
+
+  const int HH = H * HD;
+  const float c = a.scale * LOG2E;
+  const bf16_t* qkv = (const bf16_t*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  const bf16_t* O = (const bf16_t*)a.o + (int64_t)b * n * a.ld_o + h * HD;
+  const bf16_t* dO = (const bf16_t*)a.dout + (int64_t)b * n * a.ld_o + h * HD;
+  const float* lse = a.lse + ((int64_t)b * H + h) * n;
+
+  // ---- prologue: every global load of the workgroup issued before the first
+  // use (row indices clamped, out-of-range values selected to zero afterwards)
+  // this wave's key chunk: K (scaled by c: S comes out in log2 units), V as
+  // B-operand row fragments, K^T as the A operand of dQ^T in the permuted key
+  // order of pack8 / dst_frag
+  const int kbase = 32 * wave;
+  v8s kf[2], vf[2], kT[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = min(kbase + 16 * kt + l15, n - 1);
+    const bf16_t* kr = qkv + (int64_t)key * a.ld_qkv + HH + h * HD + 8 * g;
+    kf[kt] = *(const v8s*)kr;
+    vf[kt] = *(const v8s*)(kr + HH);
+  }
+  bf16_t kraw[2][8];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int key = min(kbase + 16 * (j >> 2) + 4 * g + (j & 3), n - 1);
+      kraw[dt][j] = qkv[(int64_t)key * a.ld_qkv + HH + h * HD + 16 * dt + l15];
+    }
+  // Q, dO, O chunks: thread -> chunk slots tid and tid + NTH (4 per row)
+  v4u vq[2], vd[2], vo[2];
+  float ls[2];
+  const int cc = threadIdx.x & 3;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = (threadIdx.x + u * NTH) >> 2, rc = min(row, n - 1);
+    vq[u] = *(const v4u*)(qkv + (int64_t)rc * a.ld_qkv + h * HD + 8 * cc);
+    vd[u] = *(const v4u*)(dO + (int64_t)rc * a.ld_o + 8 * cc);
+    vo[u] = *(const v4u*)(O + (int64_t)rc * a.ld_o + 8 * cc);
+    ls[u] = lse[rc];
+  }
+  for (int i = threadIdx.x * 4; i < npad * 32; i += 4 * NTH) *(v4f*)(dQi + i * 4) = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < 2 * NW * 3 * HD; i += NTH) cs[i] = 0.f;
+  ASTAMP(6);
+  float vs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // v-bias: column sums of dO
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = (threadIdx.x + u * NTH) >> 2;
+    const bool ok = row < n;
+    const v4u z = {0, 0, 0, 0};
+    const v4u q = ok ? vq[u] : z, d = ok ? vd[u] : z;
+    *(v4u*)(Qi + I::chunk(row, cc)) = q;
+    *(v4u*)(Di + I::chunk(row, cc)) = d;
+    float dd = chunk_dot<bf16_t>(d, ok ? vo[u] : z);
+    dd += __shfl_xor(dd, 1, 64);
+    dd += __shfl_xor(dd, 2, 64);
+    if (cc == 0) {
+      Dv[row] = -dd;
+      L2[row] = ok ? -ls[u] : -1.0e30f;   // S' = c S: the exponent is S' - lse2
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vs[2 * j] += __uint_as_float(d[j] << 16);
+      vs[2 * j + 1] += __uint_as_float(d[j] & 0xffff0000u);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) vs[j] += __shfl_xor(vs[j], o, 64);
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const bool kok = kbase + 16 * kt + l15 < n;
+    v8s t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = kok ? (short)f2bf(c * bf2f((bf16_t)kf[kt][j])) : (short)0;
+    kf[kt] = t;
+    vf[kt] = kok ? vf[kt] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      kT[dt][j] = kbase + 16 * (j >> 2) + 4 * g + (j & 3) < n ? (short)kraw[dt][j] : (short)0;
+  ASTAMP(7);
+  __syncthreads();
+  if (a.colsum_partial && lane < 4)   // after the barrier that ends the zero fill of cs
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[wave * 3 * HD + 2 * HD + 8 * cc + j] = vs[j];
+  ASTAMP(1);
+
+  // per-lane LDS offsets; a round adds its query-chunk base (q0 is a multiple
+  // of 32, so every swizzle below depends on the lane only)
+  const int p_ = lane & 3;
+  const int qq_ = (lane >> 2) & 3;
+  const int o_rf = I::chunk(l15, g);                     // Q / dO row fragment, + 1024 for u = 1
+  int o_tr[2];                                           // Q / dO transposed, + 1024 for h = 1
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int unit = 4 * dt + p_;
+    o_tr[dt] = I::chunk(4 * g + qq_, unit >> 1) + ((unit & 1) << 3);
+  }
+  int o_dq[2];                                           // dQ f32, + 2048 for u = 1
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) o_dq[dt] = dq_off(l15, 4 * dt + g);
+  int o_sw[2], o_sr[2];                                  // dS tile write (+ 1024 kt = 1) / read (+ 1024 h = 1)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    o_sw[u] = dst_off(l15, 4 * u + g);
+    o_sr[u] = dst_off(4 * g + qq_, 4 * u + p_);
+  }
+
+  v4f dv[2][2], dk[2][2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) { dv[kt][dt] = v4f{0, 0, 0, 0}; dk[kt][dt] = v4f{0, 0, 0, 0}; }
+
+  for (int r = 0; r < NC; ++r) {
+    int qc = wave + r;
+    qc = qc >= NC ? qc - NC : qc;
+    const int q0 = qc * 32;
+    const char* Qr = Qi + q0 * 64;
+    const char* Dr = Di + q0 * 64;
+    v8s qf[2], df[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      qf[u] = *(const v8s*)(Qr + o_rf + 1024 * u);
+      df[u] = *(const v8s*)(Dr + o_rf + 1024 * u);
+    }
+    // transposed Q / dO fragments (A operands of dK^T / dV^T): rows q0..q0+31
+    v8s qT[2], dT[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Qr + o_tr[dt]));
+      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Qr + o_tr[dt] + 1024));
+      v4s y0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Dr + o_tr[dt]));
+      v4s y1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Dr + o_tr[dt] + 1024));
+      qT[dt] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+      dT[dt] = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    v4f l2[2], dvr[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      l2[u] = *(const v4f*)(L2 + q0 + 16 * u + 4 * g);
+      dvr[u] = *(const v4f*)(Dv + q0 + 16 * u + 4 * g);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      v4f P[2], dS[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // S' - lse2 [q = 4g+i][key = lane&15] and dP - Dv, row constants as the
+        // initial accumulators
+        const v4f s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[u], kf[kt], l2[u], 0, 0, 0);
+        const v4f dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[u], vf[kt], dvr[u], 0, 0, 0);
+        // P clamped to [0, 1] by the exp's output modifier (free): softmax
+        // probabilities never exceed 1, and a padding key (zero K row: S' = 0,
+        // P = 2^-lse2) can then never overflow into 0 * inf = NaN in dQ
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          P[u][i] = fminf(fmaxf(__builtin_amdgcn_exp2f(s[i]), 0.f), 1.f);
+          dS[u][i] = P[u][i] * dp[i];
+        }
+        const v2u pk = {pack2bf(dS[u][0], dS[u][1]), pack2bf(dS[u][2], dS[u][3])};
+        *(v2u*)(myds + o_sw[u] + 1024 * kt) = pk;
+      }
+      const v8s pp = pack8(P[0], P[1]), ps = pack8(dS[0], dS[1]);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        dv[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dT[dt], pp, dv[kt][dt], 0, 0, 0);
+        dk[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT[dt], ps, dk[kt][dt], 0, 0, 0);
+      }
+    }
+    // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] for this wave's 32 keys
+    char* dQr = dQi + q0 * 128;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, myds + o_sr[u]));
+      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, myds + o_sr[u] + 1024));
+      const v8s bds = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        v4f* pq = (v4f*)(dQr + o_dq[dt] + 2048 * u);
+        *pq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kT[dt], bds, *pq, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  ASTAMP(2);
+
+  bf16_t* dqkv = (bf16_t*)a.dqkv + (int64_t)b * a.n * a.ld_dqkv;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int key = kbase + 16 * kt + l15;
+    if (key < n) {
+      bf16_t* rowp = dqkv + (int64_t)key * a.ld_dqkv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        st4<bf16_t>(rowp + HH + 16 * dt + 4 * g, dk[kt][dt] * a.scale);
+        st4<bf16_t>(rowp + 2 * HH + 16 * dt + 4 * g, dv[kt][dt]);
+      }
+    }
+  }
+  ASTAMP(3);
+  // dQ rows: thread -> (row, 4 columns); q-bias partial per (row group, column)
+  float cq[4] = {0.f, 0.f, 0.f, 0.f};
+  const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3, nrg = NTH >> 3;
+  for (int row = rg; row < n; row += nrg) {
+    const v4f v = *(const v4f*)(dQi + dq_off(row, c4)) * a.scale;
+    st4<bf16_t>(dqkv + (int64_t)row * a.ld_dqkv + h * HD + 4 * c4, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cq[i] += v[i];
+  }
+  ASTAMP(4);
+  if (a.colsum_partial) {
+    // reduce the row groups of a wave (lanes with equal c4) by shuffles, then
+    // one partial row per wave in cs
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) cq[i] += __shfl_xor(cq[i], o, 64);
+    if (lane < 8)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cs[(NW + wave) * 3 * HD + 4 * c4 + i] = cq[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * HD; i += NTH) {
+      float sum = 0.f;
+      for (int w = 0; w < 2 * NW; ++w) sum += cs[w * 3 * HD + i];
+      const int part = i / HD, d = i % HD;
+      a.colsum_partial[(int64_t)b * 3 * HH + part * HH + h * HD + d] = sum;
+    }
+  }
+  ASTAMP(5);
+}
+
+size_t bwd_diag_lds(int n) {
+  const int npad = (n + 31) & ~31, nw = npad / 32;
+  return (size_t)2 * npad * Img<bf16_t, DIAG_HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 128 +
+         (size_t)nw * 2048 + (size_t)2 * nw * 3 * DIAG_HD * 4;
+}
+
 template <typename T, int HD> size_t fwd_lds(int n) {
   const int npad = (n + 63) & ~63;
   return (size_t)2 * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
@@ -717,6 +1026,19 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   }
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   dim3 grid((unsigned)(a.B * a.H));
+  if constexpr (std::is_same<T, bf16_t>::value && HD == DIAG_HD) {
+    // one-pass diagonal backward (MAECLIP_ATTN_DIAG=0 turns it off)
+    const char* e = getenv("MAECLIP_ATTN_DIAG");
+    const int npad = (a.n + 31) & ~31;
+    if (bwd && npad <= 256 && !(e && *e == '0')) {
+      const size_t ld = bwd_diag_lds(a.n);
+      if (ld > 65536)
+        (void)hipFuncSetAttribute((const void*)attn_bwd_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ld);
+      hipLaunchKernelGGL(attn_bwd_diag_kernel, grid, dim3(2 * npad), ld, s, a);
+      MC_CHECK_LAUNCH("maeclip_attn_bwd(diag)");
+      return 0;
+    }
+  }
   if (bwd) {
     // bf16, opt-in (MAECLIP_ATTN_SDS=1): keep dS in LDS between the two phases
     // when the n x n image fits. Measured slower on MI355X at the path's shapes

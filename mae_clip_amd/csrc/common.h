@@ -69,8 +69,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 h = (__bf16)f;
   return __builtin_bit_cast(bf16_t, h);
 }
+// two f32 -> packed bf16 pair (a low) in ONE v_cvt_pk_bf16_f32 (the
+// or-of-two-casts form costs two conversions and a v_or_b32_sdwa)
+typedef __bf16 mc_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float mc_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack2bf(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((mc_f32x2){a, b}, mc_bf16x2));
 }
 
 template <typename T> __device__ __forceinline__ float ld_as_f(const T* p);

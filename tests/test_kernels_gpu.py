@@ -95,21 +95,26 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
-@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds"])
+@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
                                    (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32), (1, 577, 2, 32),
-                                   (2, 145, 2, 64)])
+                                   (2, 145, 2, 64), (2, 256, 2, 32)])
 def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     """fp32 parity mode holds two [n][hd] f32 images at a time in the
     backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well. bf16
     backward variants: four LDS images ("four"), two images with K/V (phase 1)
     and Q/dO (phase 2) tiles from HBM ("two", picked when it fits more
     workgroups per CU; "two3": its 3-workgroups-per-CU register budget at
-    hd = 32), dS kept in LDS between the phases ("sds", opt-in)."""
+    hd = 32), dS kept in LDS between the phases ("sds", opt-in), one-pass
+    diagonal schedule with dQ accumulated in LDS ("diag": bf16, hd = 32,
+    n <= 256; the default there)."""
     B, n, H, hd = shape
     if dtype == torch.float32 and (n > 256 or mode != "four"):
         pytest.skip("fp32 parity mode: n <= 256, one variant")
+    if mode == "diag" and (dtype == torch.float32 or hd != 32 or n > 256):
+        pytest.skip("diagonal backward: bf16, hd = 32, n <= 256")
+    monkeypatch.setenv("MAECLIP_ATTN_DIAG", "1" if mode == "diag" else "0")
     monkeypatch.setenv("MAECLIP_ATTN_TWO", {"two": "1", "two3": "3"}.get(mode, "0"))
     if mode == "sds":
         # bf16 backward keeps dS in LDS for dQ instead of recomputing S/dP (opt-in)

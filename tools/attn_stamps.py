@@ -33,6 +33,10 @@ for colsum in (False, True):
         d = s[:, :, k + 1] - s[:, :, k]
         print(f"  {names[k]:9s} per wave p10/50/90 {np.percentile(d,10):7.0f} {np.median(d):7.0f} {np.percentile(d,90):7.0f}"
               f"   wave-max median {np.median(d.max(1)):7.0f}")
+    if (s[:, :, 6] > 0).all():
+        for nm, (x, y) in (("pro:loads+zero", (0, 6)), ("pro:lds+shfl", (6, 7)), ("pro:barrier", (7, 1))):
+            d = s[:, :, y] - s[:, :, x]
+            print(f"  {nm:15s} per wave p10/50/90 {np.percentile(d,10):7.0f} {np.median(d):7.0f} {np.percentile(d,90):7.0f}")
     per_wave_p1 = np.median(s[:, :, 2] - s[:, :, 1], axis=0)
     print("  phase1 median by wave:", per_wave_p1.astype(int).tolist())
     starts = np.sort(wg_start)
