@@ -162,8 +162,9 @@ class KernelTimer:
     torch-ROCm refuses event-record nodes ("External events are disallowed in
     rocm"), so the launch is bracketed by two 1-lane timestamp kernels on the
     same stream (maeclip_timestamp: s_memrealtime, 100 MHz) that are captured
-    with it; every replay re-times it and harvest() collects the spans after
-    each timed step."""
+    with it; every replay re-times it, snapshot() queues a device copy of the
+    spans right after the replay's launch (no host sync between steps) and
+    harvest() reads them all after the timed loop."""
 
     def __init__(self):
         self.records = {}
@@ -171,6 +172,7 @@ class KernelTimer:
         self.only = None     # timed region: bracket only this key's launches
         self.captured = []   # (key, flops, slot) bracketed inside the graph
         self.ts = None       # device int64 [2 * slots] timestamps
+        self.snaps = []      # per timed replay: device copies of ts
 
     def hook(self, key, flops, nbytes, launch):
         if not self.active or (self.only is not None and key != self.only):
@@ -199,15 +201,25 @@ class KernelTimer:
         e.record()
         self.records.setdefault(key, [flops, nbytes, []])[2].append((s, e))
 
+    def snapshot(self):
+        """Right after a replay is launched: queue a device copy of its
+        timestamps (stream-ordered after the replay, no host sync), so the
+        timed loop's host turnaround between steps carries no D2H read."""
+        if self.captured:
+            self.snaps.append(self.ts.clone())
+
     def harvest(self):
-        """After a synchronised replay: add the captured launches' durations (ms)."""
-        if not self.captured:
+        """After the timed loop: add the captured launches' durations (ms) of
+        every snapshot (one D2H copy for the whole run)."""
+        snaps, self.snaps = self.snaps, []
+        if not self.captured or not snaps:
             return
         from mae_clip_amd import _lib
         khz = float(_lib.lib().maeclip_wallclock_khz()) or 100000.0
-        t = self.ts.view(-1, 2).cpu()
-        for key, flops, nbytes, i in self.captured:
-            self.records.setdefault(key, [flops, nbytes, []])[2].append(float(t[i, 1] - t[i, 0]) / khz)
+        for t in torch.stack(snaps).cpu():
+            t = t.view(-1, 2)
+            for key, flops, nbytes, i in self.captured:
+                self.records.setdefault(key, [flops, nbytes, []])[2].append(float(t[i, 1] - t[i, 0]) / khz)
 
     def table(self, steps, file):
         rows = []
@@ -348,10 +360,11 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        timer.snapshot()
         loss.item()  # main.py:64 syncs every step
-        timer.harvest()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timer.harvest()
     timer.active = False
     if use_dp:
         dist.barrier()

@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
   const int b = bid / H, h = bid % H;
   const int npad = (n + 63) & ~63;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  ASTAMP(0);
   char* Kimg = smem;
   char* Vimg = smem + npad * I::ROWB;
   float* kmask = (float*)(smem + 2 * npad * I::ROWB);
@@ -287,6 +288,7 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
     kmask[k] = mk;
   }
   __syncthreads();
+  ASTAMP(1);
 
   const float c = a.scale * LOG2E;
   const bool drop = a.dropout_p > 0.f;
@@ -376,7 +378,9 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
       for (int dt = 0; dt < HD / 16; ++dt) st4<T>(orow + 16 * dt + 4 * g, o[dt] * inv);
       if (g == 0 && a.lse) a.lse[((int64_t)b * H + h) * n + q] = m + log2f(lsum);
     }
+    if (qt == wave) ASTAMP(2);
   }
+  ASTAMP(3);
 }
 
 // ============================================================== backward

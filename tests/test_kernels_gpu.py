@@ -553,3 +553,19 @@ def test_image_preprocess_resize_bit_exact(dev):
     ref = preprocess_ref(ims + [crop.cpu().numpy()], S)
     assert out.shape == (len(dev_ims), 3, S, S)
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("shape", [(64, 50, 12, 64), (8, 197, 16, 32), (4, 197, 12, 64), (16, 25, 12, 64)])
+def test_attention_deterministic(dev, shape):
+    """fwd and bwd are bitwise reproducible (no atomics; fixed reduction order)."""
+    B, n, H, hd = shape
+    qkv = _rand((B * n, 3 * H * hd), torch.bfloat16, dev, seed=31)
+    dout = _rand((B * n, H * hd), torch.bfloat16, dev, seed=32)
+    runs = []
+    for _ in range(3):
+        o, lse = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5)
+        dq, part = K.attn_bwd(qkv, o, dout, lse, B, n, H, hd, hd ** -0.5)
+        runs.append((o.clone(), lse.clone(), dq.clone(), part.clone()))
+    for r in runs[1:]:
+        for x, y in zip(r, runs[0]):
+            assert torch.equal(x, y)
