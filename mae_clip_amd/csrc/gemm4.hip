@@ -373,12 +373,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          float sv = csum[ni][r];
-          sv += __shfl_xor(sv, 1, 64);
-          sv += __shfl_xor(sv, 2, 64);
-          sv += __shfl_xor(sv, 4, 64);
-          sv += __shfl_xor(sv, 8, 64);
-          csum[ni][r] = sv;
+          csum[ni][r] = row16_sum(csum[ni][r]);
         }
       const int mrow = m0 + 128 * wm + 64 * hh;
       if ((lane & 15) == 0 && mrow < M) {

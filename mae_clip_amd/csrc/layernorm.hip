@@ -121,9 +121,11 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
   load_row<NC, float>(gm, a.gamma, D, lane);
 
   for (int64_t row = (int64_t)blockIdx.x * (NTH / 64) + wave; row < a.M; row += (int64_t)gridDim.x * (NTH / 64)) {
-    float dy[NC][4], x[NC][4];
+    // every load of the row issued together (one HBM round trip per row)
+    float dy[NC][4], x[NC][4], dr[NC][4];
     load_row<NC, GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
     load_row<NC, XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
+    if (a.dres) load_row<NC, float>(dr, a.dres + row * a.lddx, D, lane);
     const float mean = a.mean[row], rstd = a.rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -140,8 +142,6 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
       }
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
-    float dr[NC][4];
-    if (a.dres) load_row<NC, float>(dr, a.dres + row * a.lddx, D, lane);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int e = c * 256 + lane * 4;
