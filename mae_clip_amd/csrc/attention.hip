@@ -715,7 +715,8 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   float* Dv = L2 + npad;
   char* dQi = (char*)(Dv + npad);                 // f32 [npad][32]
   char* dst = dQi + npad * 128;                   // NW x [32 keys][32 q] bf16
-  float* cs = (float*)(dst + NW * 2048);          // [2 NW][3 HD] bias partials
+  float* csv = (float*)(dst + NW * 2048);         // [4 NW][HD] v-bias partials (one row per 16-lane row)
+  float* csq = csv + 4 * NW * HD;                 // [4 NW][HD] q-bias partials
   char* myds = dst + wave * 2048;
   ASTAMP(0);
 
@@ -761,7 +762,6 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     ls[u] = lse[rc];
   }
   for (int i = threadIdx.x * 4; i < npad * 32; i += 4 * NTH) *(v4f*)(dQi + i * 4) = v4f{0.f, 0.f, 0.f, 0.f};
-  for (int i = threadIdx.x; i < 2 * NW * 3 * HD; i += NTH) cs[i] = 0.f;
   ASTAMP(6);
   float vs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // v-bias: column sums of dO
 #pragma unroll
@@ -773,8 +773,8 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     *(v4u*)(Qi + I::chunk(row, cc)) = q;
     *(v4u*)(Di + I::chunk(row, cc)) = d;
     float dd = chunk_dot<bf16_t>(d, ok ? vo[u] : z);
-    dd += __shfl_xor(dd, 1, 64);
-    dd += __shfl_xor(dd, 2, 64);
+    dd += dpp_mov<0xB1>(dd);   // the row's 4 chunks are one lane quad
+    dd += dpp_mov<0x4E>(dd);
     if (cc == 0) {
       Dv[row] = -dd;
       L2[row] = ok ? -ls[u] : -1.0e30f;   // S' = c S: the exponent is S' - lse2
@@ -785,10 +785,13 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
       vs[2 * j + 1] += __uint_as_float(d[j] & 0xffff0000u);
     }
   }
+  // lanes cc, cc + 4, cc + 8, cc + 12 of each 16-lane row: row_shr 4, 8 (DPP)
+  // leave the row's sum for chunk cc in lane 12 + cc
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int o = 4; o < 64; o <<= 1) vs[j] += __shfl_xor(vs[j], o, 64);
+  for (int j = 0; j < 8; ++j) {
+    vs[j] += dpp_mov<0x114>(vs[j]);
+    vs[j] += dpp_mov<0x118>(vs[j]);
+  }
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const bool kok = kbase + 16 * kt + l15 < n;
@@ -805,9 +808,9 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
       kT[dt][j] = kbase + 16 * (j >> 2) + 4 * g + (j & 3) < n ? (short)kraw[dt][j] : (short)0;
   ASTAMP(7);
   __syncthreads();
-  if (a.colsum_partial && lane < 4)   // after the barrier that ends the zero fill of cs
+  if (a.colsum_partial && (lane & 15) >= 12)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cs[wave * 3 * HD + 2 * HD + 8 * cc + j] = vs[j];
+    for (int j = 0; j < 8; ++j) csv[(4 * wave + (lane >> 4)) * HD + 8 * cc + j] = vs[j];
   ASTAMP(1);
 
   // per-lane LDS offsets; a round adds its query-chunk base (q0 is a multiple
@@ -937,18 +940,21 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   if (a.colsum_partial) {
     // reduce the row groups of a wave (lanes with equal c4) by shuffles, then
     // one partial row per wave in cs
+    // lanes c4 and c4 + 8 of each 16-lane row (row_shr 8): the row's sum in lane 8 + c4
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) cq[i] += dpp_mov<0x118>(cq[i]);
+    if ((lane & 15) >= 8)
 #pragma unroll
-      for (int o = 8; o < 64; o <<= 1) cq[i] += __shfl_xor(cq[i], o, 64);
-    if (lane < 8)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) cs[(NW + wave) * 3 * HD + 4 * c4 + i] = cq[i];
+      for (int i = 0; i < 4; ++i) csq[(4 * wave + (lane >> 4)) * HD + 4 * c4 + i] = cq[i];
     __syncthreads();
+    // q | k | v bias partials of this (sample, head); k is identically zero
     for (int i = threadIdx.x; i < 3 * HD; i += NTH) {
-      float sum = 0.f;
-      for (int w = 0; w < 2 * NW; ++w) sum += cs[w * 3 * HD + i];
       const int part = i / HD, d = i % HD;
+      float sum = 0.f;
+      if (part != 1) {
+        const float* src = part == 0 ? csq : csv;
+        for (int w = 0; w < 4 * NW; ++w) sum += src[w * HD + d];
+      }
       a.colsum_partial[(int64_t)b * 3 * HH + part * HH + h * HD + d] = sum;
     }
   }
@@ -958,7 +964,7 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
 size_t bwd_diag_lds(int n) {
   const int npad = (n + 31) & ~31, nw = npad / 32;
   return (size_t)2 * npad * Img<bf16_t, DIAG_HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 128 +
-         (size_t)nw * 2048 + (size_t)2 * nw * 3 * DIAG_HD * 4;
+         (size_t)nw * 2048 + (size_t)8 * nw * DIAG_HD * 4;
 }
 
 template <typename T, int HD> size_t fwd_lds(int n) {
