@@ -50,9 +50,24 @@ __device__ uint64_t g_stamps[256 * 8 * 2 * 4];
 constexpr int HALF = 16384;          // bytes per half image (128 rows/cols x 64 k x bf16)
 constexpr int BUF = 4 * HALF;        // one K-tile
 constexpr int LDS_BYTES = 2 * BUF;   // 128 KiB
+// BM = 192 (plain launches, KC A operand): 96-row A halves (12 KiB), waves own
+// 96 x 64 output blocks (3 x 4 fragments per quadrant row), 6 row fragments;
+// chosen when it needs fewer full-tile rounds of the grid (encoder N = 768
+// shapes: 201 tiles of 192 x 256 instead of 150 of 256 x 256 on 256 CUs)
+template <int BM> struct TileM {
+  static constexpr int MI = BM / 64;                 // A fragments per wave per half
+  static constexpr int HALF_A = BM / 2 * 128;        // bytes per A half image
+  static constexpr int BUF_T = 2 * HALF_A + 2 * HALF;
+  static constexpr int LDS_T = 2 * BUF_T;
+  __device__ static __forceinline__ int hoff(int h) { return h < 2 ? h * HALF_A : 2 * HALF_A + (h - 2) * HALF; }
+};
 
 // local index l (0..127) of a half -> offset inside the 256-wide block tile
-__device__ __forceinline__ int amap(int l, int sub) { return (l & 63) + ((l >> 6) << 7) + (sub << 6); }
+template <int BM = 256>
+__device__ __forceinline__ int amap(int l, int sub) {
+  if constexpr (BM == 256) return (l & 63) + ((l >> 6) << 7) + (sub << 6);
+  else return (l < 48 ? l : l + 48) + sub * 48;   // local row l of a 96-row half
+}
 __device__ __forceinline__ int bmap(int l, int sub) { return (l & 31) + ((l >> 5) << 6) + (sub << 5); }
 
 // Operand DMA through buffer descriptors (buffer_load_dwordx4 ... lds): the
@@ -70,13 +85,13 @@ __device__ __forceinline__ rsrc_t make_rsrc(const char* base, int64_t bytes) {
 }
 
 // per-lane byte offset of wave-instruction i (0, 1) of half `sub` (0, 1) of an operand
-template <int LAY, bool ISA, int ESZ = 2>
+template <int LAY, bool ISA, int ESZ = 2, int BM = 256>
 __device__ __forceinline__ int half_voffset(int64_t ld, int sub, int i, int wave, int lane) {
   const int q = i * 8 + wave;
   if (LAY == LAY_KC) {
     const int r = q * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int g = ISA ? amap(r, sub) : bmap(r, sub);
+    const int g = ISA ? amap<BM>(r, sub) : bmap(r, sub);
     return (int)(g * ld * ESZ) + c * 16;
   } else {
     const int kr = q * 4 + (lane >> 4);
@@ -137,20 +152,20 @@ __device__ __forceinline__ v8i cat_frag(v8s a, v8s b) {
   const v4i x = __builtin_bit_cast(v4i, a), y = __builtin_bit_cast(v4i, b);
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
-template <int F8>
-__device__ __forceinline__ void quad_mma(v4f (&acc)[8][4], int i0, int j0, const v8s (&fbq)[2][2],
-                                         const v8s (&fa)[4][2]) {
+template <int F8, int MI>
+__device__ __forceinline__ void quad_mma(v4f (&acc)[2 * MI][4], int i0, int j0, const v8s (&fbq)[2][2],
+                                         const v8s (&fa)[MI][2]) {
   if constexpr (F8 == 0) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fbq[j][ks], fa[i][ks], acc[i0 + i][j0 + j], 0, 0, 0);
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const v8i a8 = cat_frag(fa[i][0], fa[i][1]);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -173,9 +188,10 @@ __device__ __forceinline__ void quad_mma(v4f (&acc)[8][4], int i0, int j0, const
 // two row fragments is issued BEFORE the stores of the previous chunk, and the
 // stores themselves are never waited for here (they drain behind the next
 // tile's main loop, see the counted wait at the tile start).
-__device__ __forceinline__ void swap_pairs(v4f (&acc)[8][4]) {
+template <int NI8 = 8>
+__device__ __forceinline__ void swap_pairs(v4f (&acc)[NI8][4]) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NI8; ++i)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
@@ -225,10 +241,11 @@ __device__ __forceinline__ void epilogue4_tile(float* __restrict__ t, v4f (&acc)
 
 // sa / sb (fp8 only): per-row dequantisation scale of A [M] and per-column
 // scale of B [N]; the product scales the accumulator before alpha / bias.
-template <typename OutT, int EPI, bool F8 = false>
-__device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&acc)[8][4], int64_t z, int m0, int n0,
-                                          int wm, int wn, int lane, const float* __restrict__ sa = nullptr,
+template <typename OutT, int EPI, bool F8 = false, int BM = 256>
+__device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&acc)[BM / 32][4], int64_t z, int m0,
+                                          int n0, int wm, int wn, int lane, const float* __restrict__ sa = nullptr,
                                           const float* __restrict__ sb = nullptr) {
+  constexpr int NCH = BM / 32;   // row fragments (chunks) per wave: 8 (BM 256) or 6 (BM 192)
   constexpr bool LOAD_AUX = EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   constexpr bool LOAD_RES = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   const int M = (int)args.M, N = (int)args.N;
@@ -238,7 +255,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
   OutT* __restrict__ C = (OutT*)args.C + off;
   const float alpha = args.alpha, beta = args.beta;
   const bool has_res = LOAD_RES && args.resid != nullptr;
-  const int rbase = m0 + 128 * wm + (lane & 15);
+  const int rbase = m0 + (BM / 2) * wm + (lane & 15);   // + 16 i (row fragment i = chunk)
   const int cb0 = n0 + 64 * wn + 16 * (g & 1) + 8 * (g >> 1);   // + 32 ni
   v4f bias8[2][2];
 #pragma unroll
@@ -258,7 +275,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = c, ni = q;
-      const int m = min(rbase + 64 * (i >> 2) + 16 * (i & 3), M - 1);
+      const int m = min(rbase + 16 * i, M - 1);
       const int n = min(cb0 + 32 * ni, N - 8);
       if (LOAD_AUX) ax[buf][q] = *(const v4u*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + n);
       if (LOAD_RES && has_res) {
@@ -278,13 +295,13 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
     for (int c = 0; c < PF - 1; ++c) load_chunk(c, c);
   }
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    if ((LOAD_AUX || LOAD_RES) && c + PF - 1 < 8) load_chunk(c + PF - 1, (c + PF - 1) % PF);
+  for (int c = 0; c < NCH; ++c) {
+    if ((LOAD_AUX || LOAD_RES) && c + PF - 1 < NCH) load_chunk(c + PF - 1, (c + PF - 1) % PF);
     __builtin_amdgcn_sched_barrier(0);   // keep chunk c+1's loads ahead of chunk c's stores
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int i = c, ni = q;
-      const int m = rbase + 64 * (i >> 2) + 16 * (i & 3);
+      const int m = rbase + 16 * i;
       const int n = cb0 + 32 * ni;
       v4f lo, hi;
       if constexpr (F8) {
@@ -367,7 +384,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
         }
       }
     }
-    if ((c & 3) == 3 && args.colsum_partial) {  // one partial row per 64-row group hh = c >> 2
+    if (BM == 256 && (c & 3) == 3 && args.colsum_partial) {  // one partial row per 64-row group hh = c >> 2
       const int hh = c >> 2;
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
@@ -437,11 +454,14 @@ struct WgGroup {
 // F8: 0 = bf16 operands (K-tile 64); 1 / 2 = fp8 operands, A e4m3 / e5m2 and
 // B e4m3 (K-tile 128 = the same 128 bytes per row), per-row A scales sa[M] and
 // per-column B scales sb[N] applied in the epilogue.
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0>
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256>
 __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp,
                                            const float* __restrict__ sa = nullptr,
                                            const float* __restrict__ sb = nullptr) {
   static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
+  static_assert(BM == 256 || (BM == 192 && LA == LAY_KC && !SPLIT && !GRP), "BM 192: KC A, plain launches only");
+  using TM = TileM<BM>;
+  constexpr int MI = TM::MI;
   constexpr int ESZ = F8 ? 1 : 2;      // operand bytes per element
   constexpr int KT = 128 / ESZ;        // elements per K-tile (128 bytes per row)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -457,7 +477,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     T = gp->skw > 0 ? gp->Tdp : gp->T * gp->S;
     klen = ((gp->Mtok + gp->S - 1) / gp->S + KT - 1) / KT * KT;
   } else {
-    const int gm = ((int)args.M + 255) / 256;
+    const int gm = ((int)args.M + BM - 1) / BM;
     gn = ((int)args.N + 255) / 256;
     T = gm * gn;
     const int S = SPLIT ? args.splitk : 1;
@@ -490,7 +510,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       w.M = (int)args.M;
       w.N = (int)args.N;
       w.K = (int)args.K;
-      w.m0 = (u / gn) * 256;
+      w.m0 = (u / gn) * BM;
       w.n0 = (u % gn) * 256;
       w.slice = blockIdx.y;
       w.prob = 0;
@@ -542,19 +562,27 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        vA[sub][i] = half_voffset<LA, true, ESZ>(w.lda, sub, i, wave, lane);
+        vA[sub][i] = half_voffset<LA, true, ESZ, BM>(w.lda, sub, i, wave, lane);
         vB[sub][i] = half_voffset<LB, false, ESZ>(w.ldb, sub, i, wave, lane);
       }
   };
   // half h of K-tile t of unit w: 0 = Am0, 1 = Am1, 2 = Bn0, 3 = Bn1. The
   // K-tile advance is along the row (KC) or down the k-rows (RC).
   auto issue = [&](const Unit4& w, const int (&vA)[2][2], const int (&vB)[2][2], int t, int h) {
-    char* dst = smem + (t & 1) * BUF + h * HALF;
+    char* dst = smem + (t & 1) * TM::BUF_T + TM::hoff(h);
     const int k0 = w.kbeg + t * KT;
     if (h < 2) {
       const rsrc_t rs = LA == LAY_KC ? make_rsrc(w.A + (int64_t)w.m0 * w.lda * ESZ, ((int64_t)w.M - w.m0) * w.lda * ESZ)
                                      : make_rsrc(w.A + (int64_t)w.m0 * ESZ, ((int64_t)w.K * w.lda - w.m0) * ESZ);
-      issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? ESZ : (int)(w.lda * ESZ)), dst, wave);
+      if constexpr (BM == 256) {
+        issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? ESZ : (int)(w.lda * ESZ)), dst, wave);
+      } else {
+        // a 96-row A half is 12 wave-instructions: waves 0-3 issue two, 4-7 one
+        const int soff = k0 * ESZ;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + wave * 1024), 16, vA[h][0], soff, 0, 0);
+        if (wave < 4)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (8 + wave) * 1024), 16, vA[h][1], soff, 0, 0);
+      }
     } else {
       const rsrc_t rs = LB == LAY_KC ? make_rsrc(w.B + (int64_t)w.n0 * w.ldb * ESZ, ((int64_t)w.N - w.n0) * w.ldb * ESZ)
                                      : make_rsrc(w.B + (int64_t)w.n0 * ESZ, ((int64_t)w.K * w.ldb - w.n0) * ESZ);
@@ -577,6 +605,12 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   };
 
   bool primed = false, first = true, prev_full = false;
+  // everything but the three youngest halves (Am0, Bn0, Bn1 of one K-tile):
+  // 2 + 2 + 2 wave-instructions, or 1 + 2 + 2 for waves 4-7 at BM 192
+  auto wait_halves = [&]() {
+    if (BM == 256 || wave < 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  };
 #ifdef GEMM4_STAMPS
   // diagnostic build only: s_memtime at tile start / after the DMA wait /
   // after the K-loop / after the epilogue, waves 0 and 4 of every block
@@ -595,38 +629,43 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     offsets(u, voA, voB);
     if (nt > 0 && !primed) prologue(u);
     if (first && nt > 1) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      wait_halves();
     } else if (prev_full) {
       // This tile's DMA was issued before the previous tile's epilogue, whose
       // C stores (at least NST per wave for a full tile: 8 row fragments x 2
       // x 16-B, twice that for fp32) are the youngest vector-memory ops: wait
       // for everything older and let the stores drain behind this tile's
       // MFMAs instead of stalling every CU on HBM writes at once.
-      if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      if (BM == 256) {
+        if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else {   // 6 row fragments x 2 (bf16) or x 4 (fp32) stores
+        if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     first = false;
-    prev_full = !SPLIT && m0 + 256 <= u.M && n0 + 256 <= u.N;
+    prev_full = !SPLIT && m0 + BM <= u.M && n0 + 256 <= u.N;
     primed = false;
     SEG_BARRIER();
     if (wm == 1) SEG_BARRIER();
     STAMP(1);
 
-    v4f acc[8][4];
+    v4f acc[2 * MI][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 2 * MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-    v8s fa[4][2], fb[2][2][2];
+    v8s fa[MI][2], fb[2][2][2];
     for (int t = 0; t < nt; ++t) {
-      const char* buf = smem + (t & 1) * BUF;
+      const char* buf = smem + (t & 1) * TM::BUF_T;
       const char* hA0 = buf;
-      const char* hA1 = buf + HALF;
-      const char* hB0 = buf + 2 * HALF;
-      const char* hB1 = buf + 3 * HALF;
+      const char* hA1 = buf + TM::HALF_A;
+      const char* hB0 = buf + 2 * TM::HALF_A;
+      const char* hB1 = hB0 + HALF;
       const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
       // ---- p0: quadrant (0,0)
 #pragma unroll
@@ -634,14 +673,14 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = frag<LB>(hB0, 32 * wn + 16 * j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA0, 64 * wm + 16 * i, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA0, (BM / 4) * wm + 16 * i, ks, lane);
       if (more1) issue(u, voA, voB, t + 1, 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8>(acc, 0, 0, fb[0], fa);
+      quad_mma<F8, MI>(acc, 0, 0, fb[0], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p1: quadrant (0,1)
@@ -653,19 +692,19 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8>(acc, 0, 2, fb[1], fa);
+      quad_mma<F8, MI>(acc, 0, 2, fb[1], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p2: quadrant (1,1)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, 64 * wm + 16 * i, ks, lane);
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, (BM / 4) * wm + 16 * i, ks, lane);
       if (more2) issue(u, voA, voB, t + 2, 2);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8>(acc, 4, 2, fb[1], fa);
+      quad_mma<F8, MI>(acc, MI, 2, fb[1], fa);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p3: quadrant (1,0), operands already in VGPRs. Every LDS read of
@@ -673,7 +712,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       // K-tile starts the next unit's DMA here.
       if (more2) {
         issue(u, voA, voB, t + 2, 3);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        wait_halves();
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (!more1 && jb + 1 < njobs) {
@@ -686,13 +725,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       }
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8>(acc, 4, 0, fb[0], fa);
+      quad_mma<F8, MI>(acc, MI, 0, fb[0], fa);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 || more1) SEG_BARRIER();   // group 1 skips its very last one (it took one extra up front)
     }
     if (nt == 0 && wm == 0) SEG_BARRIER();
     STAMP(2);
-    if (GRP) {
+    if constexpr (BM != 256) {
+      epilogue4<OutT, EPI, F8 != 0, BM>(args, acc, z, m0, n0, wm, wn, lane, sa, sb);
+    } else if (GRP) {
       const WgProb& q = gp->p[u.prob];
       if (u.slot >= 0) {
         epilogue4_tile(gp->ws + (int64_t)u.slot * 65536, acc, wm, wn, lane);
@@ -721,9 +762,9 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   }
 }
 
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT>
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, int BM = 256>
 __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
-  gemm4_body<LA, LB, OutT, EPI, SPLIT, false>(args, nullptr);
+  gemm4_body<LA, LB, OutT, EPI, SPLIT, false, 0, BM>(args, nullptr);
 }
 
 // fp8 operands (maeclip_gemm_fp8): KC x KC, per-row / per-column scales
@@ -732,9 +773,9 @@ struct Gemm8Args {
   const float* sa;
   const float* sb;
 };
-template <typename OutT, int EPI, int F8>
+template <typename OutT, int EPI, int F8, int BM = 256>
 __global__ void __launch_bounds__(512) gemm4_f8_kernel(const Gemm8Args g) {
-  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8>(g.a, nullptr, g.sa, g.sb);
+  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8, BM>(g.a, nullptr, g.sa, g.sb);
 }
 
 // grouped weight gradients: RC x RC, fp32 out, no epilogue (beta only)
@@ -790,18 +831,48 @@ __global__ void __launch_bounds__(256) wgrad4_sk_reduce_kernel(const WgGroup grp
   }
 }
 
-template <int LA, int LB, typename OutT, int EPI>
-int launch4(const maeclip_gemm_args& a, hipStream_t s) {
-  const int gm = (int)((a.M + 255) / 256), gn = (int)((a.N + 255) / 256);
-  const int S = a.splitk > 1 ? a.splitk : 1;
-  auto kern = S > 1 ? gemm4_kernel<LA, LB, OutT, EPI, true> : gemm4_kernel<LA, LB, OutT, EPI, false>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+int gemm4_ncu() {
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
+  return ncu;
+}
+
+// 192-row tiles when they need fewer full-tile rounds of the persistent grid;
+// MAECLIP_GEMM_BM=256 / 192 forces one (A/B, tests)
+bool use_bm192(const maeclip_gemm_args& a, int ncu) {
+  const char* e = getenv("MAECLIP_GEMM_BM");   // 256 / 192: force (A/B, tests)
+  const int force = (e && *e) ? atoi(e) : 0;
+  if (force == 256 || a.a_layout != LAY_KC || a.splitk > 1 || a.batch > 1 || a.colsum_partial) return false;
+  const int64_t gn = (a.N + 255) / 256;
+  const int64_t t256 = (a.M + 255) / 256 * gn, t192 = (a.M + 191) / 192 * gn;
+  if (force == 192) return true;
+  // measured: a 192-row tile costs ~0.89 of a 256-row one (encoder fc2 fwd, 1 round each)
+  const double r256 = (double)((t256 + ncu - 1) / ncu), r192 = 0.89 * (double)((t192 + ncu - 1) / ncu);
+  return r192 < r256 - 1e-9;
+}
+
+template <int LA, int LB, typename OutT, int EPI>
+int launch4(const maeclip_gemm_args& a, hipStream_t s) {
+  const int gn = (int)((a.N + 255) / 256);
+  const int S = a.splitk > 1 ? a.splitk : 1;
+  const int ncu = gemm4_ncu();
+  if constexpr (LA == LAY_KC) {
+    if (use_bm192(a, ncu)) {
+      auto kern = gemm4_kernel<LA, LB, OutT, EPI, false, 192>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_T);
+      const int tiles = (int)((a.M + 191) / 192) * gn;
+      hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_T, s, a);
+      MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
+      return 0;
+    }
+  }
+  const int gm = (int)((a.M + 255) / 256);
+  auto kern = S > 1 ? gemm4_kernel<LA, LB, OutT, EPI, true> : gemm4_kernel<LA, LB, OutT, EPI, false>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
   // one block per CU (128 KiB LDS): persistent over tiles for plain launches;
   // split-K / batched launches get one block per (tile, slice, batch)
   const int tiles = gm * gn;
@@ -870,20 +941,24 @@ namespace {
 
 template <typename OutT, int EPI, int F8>
 int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStream_t s) {
-  auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  const int tiles = (int)(((a.M + 255) / 256) * ((a.N + 255) / 256));
-  const int grid = (a.batch > 1 || tiles < ncu) ? tiles : ncu;
+  const int ncu = gemm4_ncu();
   Gemm8Args g;
   g.a = a;
   g.sa = sa;
   g.sb = sb;
+  const int gn = (int)((a.N + 255) / 256);
+  if (use_bm192(a, ncu)) {
+    auto kern = gemm4_f8_kernel<OutT, EPI, F8, 192>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_T);
+    const int tiles = (int)((a.M + 191) / 192) * gn;
+    hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_T, s, g);
+    MC_CHECK_LAUNCH("maeclip_gemm_fp8(192-row tiles)");
+    return 0;
+  }
+  auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  const int tiles = (int)(((a.M + 255) / 256) * gn);
+  const int grid = (a.batch > 1 || tiles < ncu) ? tiles : ncu;
   hipLaunchKernelGGL(kern, dim3(grid, 1, (unsigned)a.batch), dim3(512), LDS_BYTES, s, g);
   MC_CHECK_LAUNCH("maeclip_gemm_fp8");
   return 0;

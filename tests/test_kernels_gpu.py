@@ -38,9 +38,33 @@ def test_gemm_layouts(dev, dtype, lay, mnk):
     assert err / scale < (2e-6 if dtype == torch.float32 else 2e-5) * math.sqrt(Kd), (err, scale)
 
 
+@pytest.mark.parametrize("b_lay", [0, 1])
+@pytest.mark.parametrize("mnk", [(12800, 768, 768), (1000, 520, 192), (50000, 512, 256), (192, 256, 64), (193, 264, 128)])
+def test_gemm_bm192(dev, b_lay, mnk, monkeypatch):
+    """192-row tiles (forced): ragged M / N, one tile, several persistent tiles per
+    block (M = 50000: 261 x 2 tiles on 256 CUs), KC x KC and KC x RC."""
+    monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    M, N, Kd = mnk
+    A = _rand((M, Kd), torch.bfloat16, dev, seed=1)
+    B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, seed=2)
+    for out in (torch.float32, torch.bfloat16):
+        C = torch.empty((M, N), device=dev, dtype=out)
+        K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, 0, b_lay, alpha=0.5)
+        ref = 0.5 * _ref_mm(A, B.t() if b_lay == 0 else B)
+        err = (C.double() - ref).abs().max().item()
+        scale = ref.abs().max().item() + 1e-6
+        assert err / scale < (2e-5 * math.sqrt(Kd) if out == torch.float32 else 1e-2), (out, err, scale)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M", [300, 700])   # fp32: 32x32-tile small kernel / 128x128 MFMA kernel
-def test_gemm_epilogues(dev, dtype, M):
+@pytest.mark.parametrize("bm", ["auto", "192"])
+def test_gemm_epilogues(dev, dtype, M, bm, monkeypatch):
+    """bm = "192": every epilogue on 192-row tiles (forced; colsum launches keep 256)."""
+    if bm == "192":
+        if dtype == torch.float32:
+            pytest.skip("192-row tiles: bf16 operands")
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
     N, Kd = 384, 256
     x = _rand((M, Kd), dtype, dev, seed=3)
     w = _rand((N, Kd), dtype, dev, scale=0.05, seed=4)
