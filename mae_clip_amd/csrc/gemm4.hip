@@ -636,9 +636,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       // x 16-B, twice that for fp32) are the youngest vector-memory ops: wait
       // for everything older and let the stores drain behind this tile's
       // MFMAs instead of stalling every CU on HBM writes at once.
+      // GELU epilogues with aux_out also store a bf16 pre-activation / GELU'
+      // per chunk: twice the bf16 stores, all younger than this tile's DMA
+      const bool two_out = (EPI == EPI_GELU || EPI == EPI_GELU_D) && args.aux_out != nullptr && !GRP;
       if (BM == 256) {
-        if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if (sizeof(OutT) == 2 && two_out) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else if (sizeof(OutT) == 2 && two_out) {
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       } else {   // 6 row fragments x 2 (bf16) or x 4 (fp32) stores
         if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
