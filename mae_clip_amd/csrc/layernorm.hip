@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
 
 int ln_bwd_grid(int64_t M) {
   int64_t g = (M + 3) / 4;
-  return (int)(g < 1024 ? g : 1024);
+  return (int)(g < 512 ? g : 512);
 }
 
 }  // namespace
