@@ -118,10 +118,16 @@ __global__ void __launch_bounds__(NTH) tokens_bwd_dy_kernel(const maeclip_tokens
   const v4f v = *(const v4f*)(a.dx + ((int64_t)b * (a.keep + 1) + 1 + j) * a.D + d);
   st4<YT>((YT*)a.dy + r * a.ldy + d, v);
 }
+#ifndef TBP_UNROLL
+#define TBP_UNROLL 8
+#endif
 // dpos[1+l] = sum_b [kept] dx[b,1+restore[b,l]] ; dpos[0] = dcls = sum_b dx[b,0]
 // One workgroup per (position, 256-column chunk): wave w sums the samples
-// b = w, w+4, ... (16-B loads, four rows in flight per lane), the four wave
-// partials are added in a fixed order through LDS (deterministic).
+// b = w, w+4, ... in ascending order. The wave first loads the restore index
+// of 64 of its samples (one per lane) and ballots which keep this position,
+// then issues the dx rows of only those, TBP_UNROLL 16-B loads in flight per lane
+// (no dependent index load per row, no loads for masked samples). The four
+// wave partials are added in a fixed order through LDS (deterministic).
 __global__ void __launch_bounds__(NTH) tokens_bwd_pos_kernel(const maeclip_tokens_args a) {
   __shared__ v4f red[NTH / 64][64];
   const int pr = blockIdx.x;  // 0..L
@@ -130,35 +136,28 @@ __global__ void __launch_bounds__(NTH) tokens_bwd_pos_kernel(const maeclip_token
   const int nt = a.keep + 1;
   v4f acc = {0.f, 0.f, 0.f, 0.f};
   if (d < a.D) {
-    int b = wave;
-    for (; b + 12 < a.B; b += 16) {
-      v4f v[4];
-      bool ok[4];
+    for (int b0 = 0; b0 < a.B; b0 += 4 * 64) {
+      const int bl = b0 + wave + 4 * lane;
+      // token row t = 1 + r of sample bl (r = -1: the cls row, for pr = 0)
+      int r = a.keep;
+      if (bl < a.B) r = pr == 0 ? -1 : (a.ids_restore ? a.ids_restore[(int64_t)bl * a.L + pr - 1] : pr - 1);
+      uint64_t m = __ballot(r < a.keep);
+      while (m) {
+        v4f v[TBP_UNROLL];
+        bool ok[TBP_UNROLL];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int bb = b + 4 * u;
-        int t = 0;
-        ok[u] = true;
-        if (pr > 0) {
-          const int r = a.ids_restore ? a.ids_restore[(int64_t)bb * a.L + pr - 1] : pr - 1;
-          ok[u] = r < a.keep;
-          t = 1 + (ok[u] ? r : 0);
+        for (int u = 0; u < TBP_UNROLL; ++u) {
+          ok[u] = m != 0;
+          const int i = ok[u] ? (int)__builtin_ctzll(m) : 0;
+          m &= m - 1;
+          const int t = 1 + __builtin_amdgcn_readlane(r, i);
+          const int bb = b0 + wave + 4 * i;
+          if (ok[u]) v[u] = *(const v4f*)(a.dx + ((int64_t)bb * nt + t) * a.D + d);
         }
-        v[u] = *(const v4f*)(a.dx + ((int64_t)bb * nt + t) * a.D + d);
-      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (ok[u]) acc += v[u];
-    }
-    for (; b < a.B; b += 4) {
-      int t = 0;
-      bool ok = true;
-      if (pr > 0) {
-        const int r = a.ids_restore ? a.ids_restore[(int64_t)b * a.L + pr - 1] : pr - 1;
-        ok = r < a.keep;
-        t = 1 + (ok ? r : 0);
+        for (int u = 0; u < TBP_UNROLL; ++u)
+          if (ok[u]) acc += v[u];
       }
-      if (ok) acc += *(const v4f*)(a.dx + ((int64_t)b * nt + t) * a.D + d);
     }
   }
   red[wave][lane] = acc;

@@ -522,12 +522,14 @@ def test_mae_loss_kernels_vs_torch(dev, dtype, cfg):
     assert (cs.double().cpu().sum(0) - pr.grad.sum((0, 1))).abs().max().item() < tolg * gs * L_
 
 
+@pytest.mark.parametrize("B", [16, 300])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype):
+def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype, B):
     """timm _pos_embed / PatchEmbed backward on the visible tokens and the HF
     decoder unshuffle backward (modeling_vit_mae.py:548-566): gathered rows
-    exact, position / mask-token / bias partial sums vs fp64."""
-    B, L_, keep, D, Dd = 16, 196, 49, 768, 512
+    exact, position / mask-token / bias partial sums vs fp64 (B = 300: more
+    samples than one 256-sample ballot chunk of tokens_bwd_pos, ragged tail)."""
+    L_, keep, D, Dd = 196, 49, 768, 512
     ids_s, ids_r, mask, _ = K.mask_ids(B, L_, keep, seed=2, step=1, sample_offset=0, device=dev)
     dx = _rand((B, keep + 1, D), torch.float32, dev, seed=61)
     dy, dpos, dcls = K.tokens_bwd(dx, ids_r, B, L_, keep, dtype)
