@@ -135,29 +135,33 @@ __global__ void __launch_bounds__(NTH) tokens_bwd_pos_kernel(const maeclip_token
   const int d = (blockIdx.y * 64 + lane) * 4;
   const int nt = a.keep + 1;
   v4f acc = {0.f, 0.f, 0.f, 0.f};
-  if (d < a.D) {
-    for (int b0 = 0; b0 < a.B; b0 += 4 * 64) {
-      const int bl = b0 + wave + 4 * lane;
-      // token row t = 1 + r of sample bl (r = -1: the cls row, for pr = 0)
-      int r = a.keep;
-      if (bl < a.B) r = pr == 0 ? -1 : (a.ids_restore ? a.ids_restore[(int64_t)bl * a.L + pr - 1] : pr - 1);
-      uint64_t m = __ballot(r < a.keep);
-      while (m) {
-        v4f v[TBP_UNROLL];
-        bool ok[TBP_UNROLL];
+  // Lane `lane` plays two roles: the 4-column chunk d of the sums, and sample
+  // b0 + wave + 4*lane of the restore-index ballot. The ballot must therefore
+  // run with all 64 lanes active whatever D is; only the dx loads are guarded
+  // by the column bound.
+  const bool dok = d < a.D;
+  for (int b0 = 0; b0 < a.B; b0 += 4 * 64) {
+    const int bl = b0 + wave + 4 * lane;
+    // token row t = 1 + r of sample bl (r = -1: the cls row, for pr = 0)
+    int r = a.keep;
+    if (bl < a.B) r = pr == 0 ? -1 : (a.ids_restore ? a.ids_restore[(int64_t)bl * a.L + pr - 1] : pr - 1);
+    uint64_t m = __ballot(r < a.keep);
+    while (m) {
+      v4f v[TBP_UNROLL];
+      bool ok[TBP_UNROLL];
 #pragma unroll
-        for (int u = 0; u < TBP_UNROLL; ++u) {
-          ok[u] = m != 0;
-          const int i = ok[u] ? (int)__builtin_ctzll(m) : 0;
-          m &= m - 1;
-          const int t = 1 + __builtin_amdgcn_readlane(r, i);
-          const int bb = b0 + wave + 4 * i;
-          if (ok[u]) v[u] = *(const v4f*)(a.dx + ((int64_t)bb * nt + t) * a.D + d);
-        }
-#pragma unroll
-        for (int u = 0; u < TBP_UNROLL; ++u)
-          if (ok[u]) acc += v[u];
+      for (int u = 0; u < TBP_UNROLL; ++u) {
+        ok[u] = m != 0;
+        const int i = ok[u] ? (int)__builtin_ctzll(m) : 0;
+        m &= m - 1;
+        const int t = 1 + __builtin_amdgcn_readlane(r, i);
+        const int bb = b0 + wave + 4 * i;
+        ok[u] = ok[u] && dok;
+        if (ok[u]) v[u] = *(const v4f*)(a.dx + ((int64_t)bb * nt + t) * a.D + d);
       }
+#pragma unroll
+      for (int u = 0; u < TBP_UNROLL; ++u)
+        if (ok[u]) acc += v[u];
     }
   }
   red[wave][lane] = acc;

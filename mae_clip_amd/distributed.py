@@ -41,6 +41,30 @@ def all_gather_rows(x, group=None):
     return out
 
 
+def check_equal_rows(n, group=None, device=None):
+    """Raise if the ranks hold different local batch sizes.
+
+    all_gather_into_tensor and the gradient row slice (rank * B, B) of the
+    sharded CLIP loss both assume every rank has the same B; a ragged last
+    batch (the reference's DataLoader keeps it, main.py:42-47) would otherwise
+    hang or fail inside RCCL. One tiny MAX all-reduce of (B, -B) per eager
+    step; skipped under graph capture (a captured step has fixed shapes on
+    every rank by construction)."""
+    if device is not None and device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        return
+    t = torch.tensor([n, -n], dtype=torch.int64, device=device)
+    if _staged(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t = h
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    hi, lo = int(t[0]), -int(t[1])
+    if hi != lo:
+        raise RuntimeError(f"data parallel: ranks hold different local batch sizes ({lo}..{hi}); "
+                           "use drop_last=True or pad the last batch so every rank has the same B")
+
+
 class GatherRowsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
@@ -72,14 +96,25 @@ class GradArena:
             off += p.numel()
         self.flat = torch.zeros(off, device=device, dtype=torch.float32)
 
+        # parameters whose slot has been handed out since the last forward
+        # (begin_forward): a parameter that reaches several backward Functions
+        # (tied weights, two forwards sharing one backward) gets its slot only
+        # once -- autograd sums the incoming gradients before AccumulateGrad,
+        # and two aliases of one buffer would sum to 2*g2 instead of g1+g2
+        self.handed = set()
+
+    def begin_forward(self):
+        self.handed.clear()
+
     def view(self, p):
         off, n, shape = self.offsets[id(p)]
         return self.flat[off:off + n].view(shape)
 
     def slot(self, p):
         e = self.offsets.get(id(p))
-        if e is None or p.grad is not None or p.dtype != torch.float32:
+        if e is None or p.grad is not None or p.dtype != torch.float32 or id(p) in self.handed:
             return None
+        self.handed.add(id(p))
         return self.view(p)
 
     def owns(self, p):

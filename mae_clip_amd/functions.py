@@ -40,7 +40,10 @@ _ARENA = [None]
 
 
 def set_grad_arena(arena):
+    """Called at the start of every forward: slots are handed out again from here."""
     _ARENA[0] = arena
+    if arena is not None:
+        arena.begin_forward()
 
 
 def _arena():
@@ -49,8 +52,9 @@ def _arena():
 
 def gout(arena, p, shape=None):
     """Output buffer for p's gradient: its arena slot (a fresh view object, so
-    autograd's AccumulateGrad adopts it without a copy) when p.grad is None,
-    else a new tensor (gradient accumulation adds it to the existing p.grad)."""
+    autograd's AccumulateGrad adopts it without a copy) when p.grad is None and
+    the slot has not been handed out since the forward, else a new tensor
+    (gradient accumulation / a second use of p: autograd adds it)."""
     if arena is not None:
         v = arena.slot(p)
         if v is not None:
@@ -499,10 +503,11 @@ class ClipLossFn(torch.autograd.Function):
         T = T.contiguous()
         rows = None
         if group is not None:
-            from .distributed import all_gather_rows, world_rank
+            from .distributed import all_gather_rows, world_rank, check_equal_rows
             world, rank = world_rank(group)
             if world > 1:
                 B = I.shape[0]
+                check_equal_rows(B, group, I.device)
                 I = all_gather_rows(I, group)
                 T = all_gather_rows(T, group)
                 rows = (rank * B, B)

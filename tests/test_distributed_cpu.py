@@ -131,3 +131,35 @@ def test_data_parallel_equals_full_batch(bucket_mb, overlap):
     # both ranks hold identical synchronised gradients
     for n in res[0][3]:
         assert torch.equal(res[0][3][n], res[1][3][n]), n
+
+
+def test_grad_arena_slot_handed_out_once():
+    """A parameter reaching two backward Functions gets its arena slot once;
+    the second request must get a fresh tensor (else autograd would sum two
+    aliases of one buffer: 2*g2 instead of g1+g2). begin_forward re-arms."""
+    from mae_clip_amd.distributed import GradArena
+    p = torch.nn.Parameter(torch.zeros(4, 3))
+    q = torch.nn.Parameter(torch.zeros(5))
+    ar = GradArena([p, q], "cpu")
+    s1 = ar.slot(p)
+    assert s1 is not None and s1.data_ptr() == ar.flat.data_ptr()
+    assert ar.slot(p) is None
+    assert ar.slot(q) is not None
+    ar.begin_forward()
+    assert ar.slot(p) is not None
+
+
+def _ragged_body(rank, world):
+    from mae_clip_amd.distributed import check_equal_rows
+    check_equal_rows(4, None, torch.device("cpu"))          # equal: passes
+    try:
+        check_equal_rows(4 + rank, None, torch.device("cpu"))
+    except RuntimeError as e:
+        return str(e)
+    return None
+
+
+def test_data_parallel_rejects_ragged_batches():
+    """ranks with different local B fail with a clear error, not a hang."""
+    res = run_ranks(_ragged_body)
+    assert all(r is not None and "different local batch sizes" in r for r in res)

@@ -558,6 +558,27 @@ def test_tokens_and_unshuffle_bwd_vs_torch(dev, dtype, B):
     assert (cs.double().cpu().sum(0) - ref_dy.sum((0, 1))).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("B", [129, 300])
+@pytest.mark.parametrize("D", [64, 192, 384, 1024])
+def test_tokens_bwd_pos_narrow_rows(dev, D, B):
+    """pos_embed / cls_token gradients when D/4 is not a multiple of 64: the
+    lanes past the last column still cast their sample's ballot vote (a lane
+    is both a column chunk and a sample of the restore-index ballot), so no
+    sample is dropped from dpos for ViT-Tiny / ViT-S widths."""
+    L_, keep = 196, 49
+    ids_s, ids_r, _, _ = K.mask_ids(B, L_, keep, seed=3, step=2, sample_offset=0, device=dev)
+    dx = _rand((B, keep + 1, D), torch.float32, dev, seed=63)
+    _, dpos, dcls = K.tokens_bwd(dx, ids_r, B, L_, keep, torch.bfloat16)
+    x64 = dx.double().cpu()
+    ref = torch.zeros(L_ + 1, D, dtype=torch.float64)
+    ref[0] = x64[:, 0].sum(0)
+    s = ids_s.cpu().long()
+    for b in range(B):
+        ref[1 + s[b, :keep]] += x64[b, 1:]
+    assert (dpos.double().cpu() - ref).abs().max().item() < 1e-4
+    assert torch.equal(dcls, dpos[0])
+
+
 
 def test_image_preprocess_resize_bit_exact(dev):
     """maeclip_image_preprocess_u8 (A.Resize INTER_LINEAR + A.Normalize +

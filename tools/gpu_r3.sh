@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-3 GPU session script: GPU tests, smoke, default bench, optional extra
+# steps selected by $STEPS (space-separated: gemmcal prof). Every GPU step has
+# its own limit and the chain stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG="${TAG:-r3}"
+STEPS="${STEPS:-tests bench}"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 480 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
+        > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
+      tail -3 gpurun_out/pytest_gpu_${TAG}.log ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 || { tail -30 gpurun_out/smoke_${TAG}.log; exit 1; }
+      tail -1 gpurun_out/smoke_${TAG}.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
+      cat gpurun_out/bench_${TAG}.json ;;
+    benchq)
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-parity --steps 20 > gpurun_out/benchq_${TAG}.json 2> gpurun_out/benchq_${TAG}.err || { tail -30 gpurun_out/benchq_${TAG}.err; exit 1; }
+      cat gpurun_out/benchq_${TAG}.json ;;
+    gemmcal)
+      timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/gemmcal_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gemmcal_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/gemmcal_${TAG}.jsonl ;;
+    gemmepi)
+      GEMM_SET=epi timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/gemmepi_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gemmepi_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/gemmepi_${TAG}.jsonl ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
+        python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
+      tail -1 gpurun_out/prof_${TAG}.log ;;
+    *)
+      echo "unknown step $s"; exit 2 ;;
+  esac
+done
