@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 3
+#define MAECLIP_ABI_VERSION 4
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -230,9 +230,12 @@ int32_t maeclip_ln_bwd_partial_rows(int64_t M);
 
 /* ------------------------------------------------------------ reductions */
 /* out[n] (+)= scale * sum_p partial[p*N + n]  (fixed order -> deterministic);
- * two passes when P > 64 (scratch: f32 [ceil(P/64)][N], may be NULL otherwise) */
+ * two passes when maeclip_colsum_scratch(P, N) > 0: scratch holds that many
+ * floats (N > 1, P > 64: [ceil(P/64)][N]; N == 1, P > 4096: ceil(P/4096)),
+ * may be NULL otherwise. */
 int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_t N, float* out, int32_t accumulate, float scale,
                               float* scratch, void* stream);
+int64_t maeclip_colsum_scratch(int64_t P, int64_t N);
 /* many independent column reductions in one launch (bias / LN-parameter
  * gradients of a whole transformer stack): out[n] (+)= scale * sum_p partial[p][n];
  * block_start = prefix sum of ceil(N/64) over the entries. */

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -161,6 +161,7 @@ _SIGS = {
     "maeclip_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_f32, c_vp, c_vp]),
     "maeclip_rows_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),
+    "maeclip_colsum_scratch": (c_i64, [c_i64, c_i64]),
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "maeclip_pool_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp]),
     "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp, c_vp]),

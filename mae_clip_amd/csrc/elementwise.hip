@@ -47,7 +47,32 @@ __global__ void __launch_bounds__(NTH) colsum_pass1_kernel(const float* __restri
   if (ph == 0 && n < N) scratch[(int64_t)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
-// single-vector sum (P large, N == 1): one workgroup, fixed-order tree
+// single-vector sum, pass 1 (P > VS_CHUNK): block b sums x[b*VS_CHUNK ..
+// +VS_CHUNK) in a fixed order (16 B per lane per iteration) -> scratch[b]
+constexpr int VS_CHUNK = NTH * 16;
+__global__ void __launch_bounds__(NTH) vec_sum_pass1_kernel(const float* __restrict__ x, int64_t P,
+                                                            float* __restrict__ scratch) {
+  __shared__ float red[NTH / 64];
+  const int64_t base = (int64_t)blockIdx.x * VS_CHUNK;
+  const int64_t end = min(base + (int64_t)VS_CHUNK, P);
+  float s = 0.f;
+  if (end - base == VS_CHUNK && ((uintptr_t)(x + base) & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < VS_CHUNK / (NTH * 4); ++i) {
+      const v4f v = *(const v4f*)(x + base + (int64_t)(i * NTH + threadIdx.x) * 4);
+      s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+  } else {
+    for (int64_t i = base + threadIdx.x; i < end; i += NTH) s += x[i];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) scratch[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// single-vector sum (N == 1): one workgroup, fixed-order tree (after pass 1
+// when P > VS_CHUNK, so the one workgroup reads at most a few hundred floats)
 __global__ void __launch_bounds__(NTH) vec_sum_kernel(const float* __restrict__ x, int64_t P, float* __restrict__ out,
                                                       int accumulate, float scale) {
   __shared__ float red[NTH / 64];
@@ -283,6 +308,15 @@ extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_
     P = (P + 63) / 64;
   }
   if (N == 1) {
+    if (P > VS_CHUNK) {
+      MC_CHECK_ARG(scratch != nullptr, "maeclip_colsum_reduce: N == 1, P > %d needs scratch [ceil(P/%d)]", VS_CHUNK,
+                   VS_CHUNK);
+      const int64_t G = (P + VS_CHUNK - 1) / VS_CHUNK;
+      hipLaunchKernelGGL(vec_sum_pass1_kernel, dim3((unsigned)G), dim3(NTH), 0, s, partial, P, scratch);
+      MC_CHECK_LAUNCH("maeclip_colsum_reduce(vec pass1)");
+      partial = scratch;
+      P = G;
+    }
     hipLaunchKernelGGL(vec_sum_kernel, dim3(1), dim3(NTH), 0, s, partial, P, out, accumulate, scale);
   } else {
     hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + NTH - 1) / NTH)), dim3(NTH), 0, s, partial, P, N, out,
@@ -294,6 +328,12 @@ extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_
 
 
 extern "C" int32_t maeclip_rows_colsum_partial_rows(int64_t M) { return rows_colsum_grid(M); }
+
+// scratch floats maeclip_colsum_reduce needs for a [P, N] partial matrix
+extern "C" int64_t maeclip_colsum_scratch(int64_t P, int64_t N) {
+  if (N == 1) return P > VS_CHUNK ? (P + VS_CHUNK - 1) / VS_CHUNK : 0;
+  return P > 64 ? (P + 63) / 64 * N : 0;
+}
 
 extern "C" int32_t maeclip_rows_colsum(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld, void* out_bf16,
                                        float* partial, void* stream) {

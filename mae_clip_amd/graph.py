@@ -83,7 +83,11 @@ class CapturedStep:
         # capture recorded the work without running it: undo its host-side counting
         self.model.step = model_step
         self.opt._advance_host_steps(-1)
-        self.graph, self.loss = g, loss
+        # detached: the captured loss must not keep the capture's autograd graph
+        # (and its AccumulateGrad nodes, bound to the capture stream) alive into
+        # later eager fallback steps or a re-capture (torch's AccumulateGrad
+        # stream-mismatch hazard); the replays still refresh its storage
+        self.graph, self.loss = g, loss.detach()
         self.hp_key = self._hparams()
         self.graph_grads = [(p, p.grad) for grp in self.opt.param_groups for p in grp["params"]]
         self.captures += 1

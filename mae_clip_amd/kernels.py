@@ -272,7 +272,8 @@ def colsum_reduce(partial, out=None, accumulate=False, scale=1.0):
     _dev(partial)
     P, N = partial.shape
     out = out if out is not None else torch.empty((N,), device=partial.device, dtype=torch.float32)
-    scratch = torch.empty(((P + 63) // 64, N), device=partial.device, dtype=torch.float32) if (N > 1 and P > 64) else None
+    ns = int(L.lib().maeclip_colsum_scratch(P, N))
+    scratch = torch.empty((ns,), device=partial.device, dtype=torch.float32) if ns > 0 else None
     _call("maeclip_colsum_reduce", partial.data_ptr(), P, N, out.data_ptr(), int(accumulate), scale, _ptr(scratch),
           _stream())
     return out

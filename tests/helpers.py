@@ -64,3 +64,17 @@ def build_pair(precision="fp32", seed=0, **overrides):
     sd = {k: v.detach().clone() for k, v in prod.state_dict().items()}
     missing, unexpected = ref.load_state_dict(sd, strict=True), None
     return prod.cuda(), ref.double()
+
+
+def record_parity(name, **vals):
+    """Append one measured deviation record (JSON line) to $MAECLIP_PARITY_OUT
+    when set (tools/gpu_r3.sh points it into gpurun_out/; the merged records
+    are committed as profiles/<round>/parity.json). Always printed as well."""
+    import json
+    import os
+    rec = dict(test=name, **{k: (float(v) if isinstance(v, (int, float)) else v) for k, v in vals.items()})
+    print("PARITY", json.dumps(rec))
+    path = os.environ.get("MAECLIP_PARITY_OUT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")

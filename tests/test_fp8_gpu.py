@@ -109,11 +109,12 @@ def test_fp8_quantisation_error_is_bounded(dev):
 def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
     """C4 shapes (ViT-L/14 @336, encoder cut to 4 blocks, B = 4; decoder 2 x 512,
     n = 577): fp8 stack GEMMs (e4m3 forward, e5m2 x e4m3 dgrad, per-token /
-    per-channel scales) vs the fp64 CPU oracle on the same weights. Tolerances:
-    loss within 3e-2 relative (the bf16 path is held to 2e-2 by
-    test_vitl14_336_shapes_bf16_vs_oracle), and every trainable gradient within
-    relative L2 error 0.15 of the bf16 path's (e4m3 operands carry 3 mantissa
-    bits against bf16's 7)."""
+    per-channel scales) and the bf16 path vs the fp64 CPU oracle (forward AND
+    backward) on the same weights. Tolerances (about 2x the values measured on
+    MI355X, profiles/r03/parity.json): loss relative FP8_TOL[0]; every
+    trainable gradient's relative L2 error vs the ORACLE's within FP8_TOL[1]
+    (bf16: BF16_C4_TOL); fp8 vs bf16 within FP8_TOL[2]."""
+    from tests.helpers import record_parity
     kw = dict(model_name="vit_large_patch14_336", size=336, image_embedding=1024, text_layers=2, mask_ratio=0.75,
               decoder_embed_dim=512, decoder_depth=2, decoder_num_heads=16, vit_depth=4)
     batch = make_batch(4, 336)
@@ -127,20 +128,40 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
         out[prec] = (loss.item(), {n: p.grad.detach().double().cpu() for n, p in prod.named_parameters()
                                    if p.requires_grad})
     ref.eval()
-    with torch.no_grad():
-        rloss = ref(dict(batch, image=batch["image"].double())).item()
+    rl = ref(dict(batch, image=batch["image"].double()))
+    rl.backward()
+    rloss = rl.item()
+    rg = {n: p.grad.detach() for n, p in ref.named_parameters() if p.grad is not None}
     l8, g8 = out["fp8"]
     lb, gb = out["bf16"]
-    print(f"fp8 loss {l8:.6f}  bf16 loss {lb:.6f}  oracle {rloss:.6f}")
-    assert abs(l8 - rloss) < 3e-2 * max(1.0, abs(rloss)), (l8, lb, rloss)
-    worst = 0.0
-    for n, gbn in gb.items():
-        assert torch.isfinite(g8[n]).all(), n
-        den = gbn.norm().item()
-        if den > 0:
-            worst = max(worst, (g8[n] - gbn).norm().item() / den)
-    print(f"worst relative L2 gradient deviation fp8 vs bf16: {worst:.4f}")
-    assert worst < 0.15, worst
+
+    def worst_rel(g, base):
+        w, wn = 0.0, None
+        for n, b in base.items():
+            assert torch.isfinite(g[n]).all(), n
+            den = b.norm().item()
+            if den > 0:
+                e = (g[n] - b).norm().item() / den
+                if e > w:
+                    w, wn = e, n
+        return w, wn
+
+    w8o, n8o = worst_rel(g8, rg)
+    wbo, nbo = worst_rel(gb, rg)
+    w8b, _ = worst_rel(g8, gb)
+    r8 = abs(l8 - rloss) / max(1.0, abs(rloss))
+    rb = abs(lb - rloss) / max(1.0, abs(rloss))
+    record_parity("vitl14_336_fp8_vs_oracle", loss_rel=r8, worst_grad_relL2=w8o, worst_grad=n8o,
+                  worst_grad_relL2_vs_bf16=w8b)
+    record_parity("vitl14_336_bf16_vs_oracle_grads", loss_rel=rb, worst_grad_relL2=wbo, worst_grad=nbo)
+    assert r8 < FP8_TOL[0], (l8, lb, rloss)
+    assert w8o < FP8_TOL[1], (w8o, n8o)
+    assert wbo < BF16_C4_TOL, (wbo, nbo)
+    assert w8b < FP8_TOL[2], w8b
+
+
+FP8_TOL = (3e-2, 0.2, 0.15)
+BF16_C4_TOL = 0.1
 
 
 def test_batched_weight_quantisation_matches_single(dev):

@@ -442,6 +442,20 @@ def test_colsum_two_pass(dev):
     assert (out.double() - part.double().sum(0)).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("P", [7, 4096, 4097, 50176, 200003])
+def test_vector_sum_two_level(dev, P):
+    """N == 1 (the MAE loss's per-patch rows): grid-wide pass 1 + one-block
+    pass 2, fixed order (bitwise reproducible), accumulate and scale."""
+    x = _rand((P, 1), torch.float32, dev, seed=44)
+    out = K.colsum_reduce(x, scale=0.5)
+    ref = x.double().sum().item() * 0.5
+    assert abs(out.item() - ref) < 1e-5 * max(1.0, x.double().abs().sum().item())
+    assert torch.equal(out, K.colsum_reduce(x, scale=0.5))
+    acc = torch.full((1,), 3.0, device=dev)
+    K.colsum_reduce(x, out=acc, accumulate=True, scale=0.5)
+    assert abs(acc.item() - (3.0 + ref)) < 1e-5 * max(1.0, x.double().abs().sum().item())
+
+
 @pytest.mark.parametrize("shape", [(4, 224, 224), (3, 32, 30), (2, 336, 336), (1, 7, 5)])
 def test_image_normalize_u8_bit_exact(dev, shape):
     """Device input pipeline (dataset.py:49, 34): uint8 HWC -> normalised fp32

@@ -4,7 +4,7 @@ vs the CPU oracle (fp64) on identical weights and inputs -- loss within 1e-3
 import pytest
 import torch
 
-from tests.helpers import build_pair, make_batch
+from tests.helpers import build_pair, make_batch, record_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -114,8 +114,14 @@ def test_vitb_parity_fp32_vs_oracle(dev, cfg):
         r_s, r_r, r_m, _ = ref.mask_for_batch(2, 0)
         assert torch.equal(ids_s.cpu().long(), r_s) and torch.equal(mask.cpu(), r_m)
     worst = _grad_errs(prod, ref)
-    print(cfg, "fp32 |dloss|", d, "worst grads", worst[:3])
+    record_parity(f"vitb_{cfg}_fp32_vs_oracle", loss_abs=d, loss_rel=d / max(1.0, abs(rloss.item())),
+                  worst_grad_maxrel=worst[0][0], worst_grad=worst[0][1])
     assert worst[0][0] < 1e-3, worst[:5]
+
+
+# (loss rel, worst gradient rel-L2) bounds for the bf16 path vs the fp64 oracle:
+# about 2x the values measured on MI355X (profiles/r03/parity.json)
+BF16_TOL = {"C1": (2e-2, 1e-1), "C2": (2e-2, 1e-1)}
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
@@ -141,9 +147,9 @@ def test_vitb_bf16_vs_oracle(dev, cfg):
         worst = max(worst, e)
         if not e < 1e-1:
             bad.append((e, name))
-    print(cfg, "bf16 loss rel", rel, "worst grad rel-L2", worst)
-    assert rel < 2e-2, (loss.item(), rloss.item())
-    assert not bad, sorted(bad, reverse=True)[:5]
+    record_parity(f"vitb_{cfg}_bf16_vs_oracle", loss_rel=rel, worst_grad_relL2=worst)
+    assert rel < BF16_TOL[cfg][0], (loss.item(), rloss.item())
+    assert worst < BF16_TOL[cfg][1], sorted(bad, reverse=True)[:5]
 
 
 def test_c0_bf16_close(dev):
@@ -262,8 +268,22 @@ def test_captured_step_partial_batch_and_lr_change(dev):
     from mae_clip_amd.optim import AdamW
     from mae_clip_amd.graph import CapturedStep
     kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    import warnings
     sizes = [8, 8, 8, 5, 8, 8, 1, 8]
     runs = []
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        _partial_runs(dev, sizes, runs, product_config, kw, CLIPModel, AdamW, CapturedStep)
+    # no AccumulateGrad node may outlive its step into a capture / eager fallback
+    assert not [w for w in caught if "AccumulateGrad" in str(w.message)], [str(w.message) for w in caught]
+    (le, me, _), (lg, mg, rg) = runs
+    assert le == lg, (le, lg)
+    assert rg.captures == 2          # initial capture + the re-capture after the lr change
+    for (n1, p1), (n2, p2) in zip(me.named_parameters(), mg.named_parameters()):
+        assert torch.equal(p1, p2), n1
+
+
+def _partial_runs(dev, sizes, runs, product_config, kw, CLIPModel, AdamW, CapturedStep):
     for captured in (False, True):
         with product_config(precision="fp32", **kw):
             torch.manual_seed(0)
@@ -278,11 +298,6 @@ def test_captured_step_partial_batch_and_lr_change(dev):
             batch = {k: v.to(dev) for k, v in make_batch(B, 32, seed=it).items()}
             losses.append(runner.step(batch).item())
         runs.append((losses, m, runner))
-    (le, me, _), (lg, mg, rg) = runs
-    assert le == lg, (le, lg)
-    assert rg.captures == 2          # initial capture + the re-capture after the lr change
-    for (n1, p1), (n2, p2) in zip(me.named_parameters(), mg.named_parameters()):
-        assert torch.equal(p1, p2), n1
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
@@ -415,3 +430,67 @@ def test_inference_find_matches(dev):
     sim = torch.nn.functional.normalize(t.double(), dim=-1) @ torch.nn.functional.normalize(emb.double(), dim=-1).T
     order = sorted(range(sim.shape[1]), key=lambda i: (-sim[0, i].item(), i))[:15][::5]
     assert idx.tolist() == order
+
+
+def test_reference_training_curve_fp32(dev):
+    """20 steps of the reference's train loop (main.py:54-66,
+    AdamW(lr 1e-3, wd 1e-3) as main.py:101-103, constant LR) at C0 with mask 0
+    (the reference's CLIP path), fp32 parity mode + the HIP AdamW, against the
+    loss sequence the reference's own CLIP.py / modules.py produced in fp64
+    (tests/golden/train_curve.npz, tools/gen_golden.py gen_train_curve) from
+    the same initial weights (checked by per-tensor sums) and batches.
+    Tolerance: |dloss| / loss <= CURVE_TOL at every step (the fp32 CPU oracle
+    itself stays within 1.4e-5 of the fp64 reference over these 20 steps)."""
+    import os
+    import numpy as np
+    from tests.helpers import C0, product_config
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.optim import AdamW
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "train_curve.npz"))
+    kw = dict(C0, mask_ratio=0.0)
+    kw.pop("batch_size")
+    torch.manual_seed(0)
+    with product_config(precision="fp32", **kw):
+        m = CLIPModel()
+    for k, v in m.state_dict().items():
+        if v.is_floating_point():
+            ref_sum = float(z["sum." + k])
+            assert abs(v.double().sum().item() - ref_sum) <= 1e-6 * (1.0 + abs(ref_sum)), k
+    m = m.to(dev).eval()
+    opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    ref = z["losses"]
+    rels = []
+    for k in range(len(ref)):
+        b = {kk: v.to(dev) for kk, v in make_batch(8, 32, seed=300 + k).items()}
+        loss = m(b)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        rels.append(abs(loss.item() - ref[k]) / abs(ref[k]))
+    record_parity("reference_train_curve_c0_fp32", steps=len(ref), worst_loss_rel=max(rels), last_loss_rel=rels[-1])
+    assert max(rels) < CURVE_TOL, rels
+
+
+CURVE_TOL = 1e-4
+
+
+def test_vitl14_336_full_depth_bf16_vs_oracle(dev):
+    """C4 model at full depth (ViT-L/14 @336: 24 encoder blocks, 8 x 512-d
+    decoder at n = 577, 6-layer text), B = 1: bf16 production loss vs the fp64
+    CPU oracle on identical weights (forward only on the oracle side)."""
+    prod, ref = build_pair("bf16", model_name="vit_large_patch14_336", size=336, image_embedding=1024,
+                           text_layers=6, mask_ratio=0.75, decoder_embed_dim=512, decoder_depth=8,
+                           decoder_num_heads=16)
+    prod.eval()
+    ref.eval()
+    batch = make_batch(1, 336, seed=21)
+    loss = prod({k: v.to(dev) for k, v in batch.items()})
+    loss.backward()
+    for n_, p in prod.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None and torch.isfinite(p.grad).all().item(), n_
+    with torch.no_grad():
+        rloss = ref(dict(batch, image=batch["image"].double())).item()
+    rel = abs(loss.item() - rloss) / max(1.0, abs(rloss))
+    record_parity("vitl14_336_full_depth_bf16_vs_oracle", loss_rel=rel, product=loss.item(), oracle=rloss)
+    assert rel < 2e-2, (loss.item(), rloss)

@@ -47,12 +47,13 @@ PROJ_DIM = 32
 class HFAvgViT(nn.Module):
     """timm.create_model(name, pretrained, num_classes=0, global_pool="avg") stand-in."""
 
-    def __init__(self):
+    def __init__(self, vit_cfg=None):
         super().__init__()
-        self.vit = ViTMAEModel(ViTMAEConfig(mask_ratio=0.0, **VIT))
+        vit_cfg = vit_cfg or VIT
+        self.vit = ViTMAEModel(ViTMAEConfig(mask_ratio=0.0, **vit_cfg))
         with torch.no_grad():
             self.vit.embeddings.initialize_weights()
-        self.fc_norm = nn.LayerNorm(VIT["hidden_size"], eps=1e-6)
+        self.fc_norm = nn.LayerNorm(vit_cfg["hidden_size"], eps=1e-6)
 
     def forward(self, x):
         B = x.shape[0]
@@ -64,16 +65,20 @@ class HFAvgViT(nn.Module):
         return self.fc_norm(h[:, 1:].mean(dim=1))
 
 
+# what the stub builds next (gen_train_curve switches these to the C0 sizes)
+STUB = {"vit": None, "text": TEXT}
+
+
 def import_reference():
     stub = types.ModuleType("timm")
-    stub.create_model = lambda name, pretrained=False, num_classes=0, global_pool="avg": HFAvgViT()
+    stub.create_model = lambda name, pretrained=False, num_classes=0, global_pool="avg": HFAvgViT(STUB["vit"])
     sys.modules["timm"] = stub
     sys.path.insert(0, REF)
     import config as RCFG  # the reference's config.py
     RCFG.projection_dim = PROJ_DIM       # bound at def time by modules.py:59-60
     import modules as RM
     import CLIP as RC
-    RM.DistilBertConfig = lambda: DistilBertConfig(**TEXT)
+    RM.DistilBertConfig = lambda: DistilBertConfig(**STUB["text"])
     RM.TextEncoder.__init__.__defaults__ = ("distilbert-base-uncased", False, False)
     RM.ImageEncoder.__init__.__defaults__ = ("vit_pico", False, True)
     return RCFG, RM, RC
@@ -93,10 +98,11 @@ def _arr(v):
     return a.astype(np.float32) if a.dtype == np.float64 else a
 
 
-def npz(name, **arrs):
+def npz(name, keep64=(), **arrs):
     os.makedirs(OUT, exist_ok=True)
     path = os.path.join(OUT, name)
-    np.savez_compressed(path, **{k: _arr(v) for k, v in arrs.items()})
+    np.savez_compressed(path, **{k: (np.asarray(v, dtype=np.float64) if k in keep64 else _arr(v))
+                                 for k, v in arrs.items()})
     print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KiB)")
 
 
@@ -247,14 +253,109 @@ def gen_clip_model(RM, RC):
     npz("clip_model.npz", **out)
 
 
+C0_VIT = dict(image_size=32, patch_size=16, num_channels=3, hidden_size=192, num_hidden_layers=12,
+              num_attention_heads=3, intermediate_size=768, hidden_act="gelu", layer_norm_eps=1e-6, qkv_bias=True,
+              hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+C0_TEXT = dict(n_layers=2)   # DistilBertConfig defaults otherwise: 768-d, 12 heads, vocab 30522
+CURVE_STEPS = 20
+
+
+def product_c0_state(seed=0):
+    """The product's own C0 initial weights (mask 0: the reference's CLIP path),
+    built on the CPU in fp32 exactly as tests/helpers.build_pair does, so the
+    GPU test can rebuild them from the seed instead of shipping 30 MB."""
+    from tests.helpers import C0, product_config
+    from mae_clip_amd.CLIP import CLIPModel
+    kw = dict(C0, mask_ratio=0.0)
+    kw.pop("batch_size")
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float32)
+    try:
+        torch.manual_seed(seed)
+        with product_config(precision="fp32", **kw):
+            prod = CLIPModel()
+    finally:
+        torch.set_default_dtype(old)
+    return {k: v.detach().clone() for k, v in prod.state_dict().items()}
+
+
+def timm_to_hf(sd, layers):
+    """product (timm names, fused qkv) -> the stub's HF ViTMAE names."""
+    out = {}
+    src, dst = "image_encoder.model.", "image_encoder.model.vit."
+    for k, v in sd.items():
+        if not k.startswith(src):
+            out[k] = v
+    out[dst + "embeddings.cls_token"] = sd[src + "cls_token"]
+    out[dst + "embeddings.position_embeddings"] = sd[src + "pos_embed"]
+    out[dst + "embeddings.patch_embeddings.projection.weight"] = sd[src + "patch_embed.proj.weight"]
+    out[dst + "embeddings.patch_embeddings.projection.bias"] = sd[src + "patch_embed.proj.bias"]
+    out[src + "fc_norm.weight"] = sd[src + "fc_norm.weight"]
+    out[src + "fc_norm.bias"] = sd[src + "fc_norm.bias"]
+    names = {"norm1": "layernorm_before", "norm2": "layernorm_after", "attn.proj": "attention.o_proj",
+             "mlp.fc1": "mlp.fc1", "mlp.fc2": "mlp.fc2"}
+    for i in range(layers):
+        b, h = f"{src}blocks.{i}.", f"{dst}layers.{i}."
+        for a, c in names.items():
+            for kind in ("weight", "bias"):
+                out[f"{h}{c}.{kind}"] = sd[f"{b}{a}.{kind}"]
+        for kind in ("weight", "bias"):
+            q, k_, v_ = sd[f"{b}attn.qkv.{kind}"].chunk(3, 0)
+            out[f"{h}attention.q_proj.{kind}"] = q
+            out[f"{h}attention.k_proj.{kind}"] = k_
+            out[f"{h}attention.v_proj.{kind}"] = v_
+    return out
+
+
+def gen_train_curve(RC):
+    """the reference's own training loop semantics
+    (main.py:54-66: model(batch), zero_grad, backward, AdamW step; AdamW(lr 1e-3,
+    wd 1e-3) over model.parameters() as main.py:101-103, constant LR because the
+    scheduler is never stepped, main.py:60-61,107) run for 20 steps on the
+    reference CLIPModel (CLIP.py / modules.py, ViT-Tiny/16 @32 stub + 2-layer
+    DistilBERT = C0, mask 0) from the product's C0 initial weights, eval mode
+    (dropout off: the product draws its own dropout masks), batch k =
+    tests.helpers.make_batch(8, 32, seed=300 + k). Stores the 20 losses and
+    per-tensor sums of the initial weights (the test's seed check)."""
+    from tests.helpers import make_batch as h_make_batch
+    STUB["vit"], STUB["text"] = C0_VIT, C0_TEXT
+    sd0 = product_c0_state(0)
+    ref = RC.CLIPModel(temperature=1.0, image_embedding=192, text_embedding=768)
+    STUB["vit"], STUB["text"] = None, TEXT
+    ref.image_projection = type(ref.image_projection)(embedding_dim=192, projection_dim=256, dropout=0.1)
+    ref.text_projection = type(ref.text_projection)(embedding_dim=768, projection_dim=256, dropout=0.1)
+    hf = {k: v.double() for k, v in timm_to_hf(sd0, 12).items()}
+    missing, unexpected = ref.load_state_dict(hf, strict=False)
+    assert not unexpected, unexpected
+    assert all(k.startswith("image_encoder.model.vit.layernorm.") for k in missing), missing
+    ref.double().eval()
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-3)
+    losses = []
+    for k in range(CURVE_STEPS):
+        b = h_make_batch(8, 32, seed=300 + k)
+        batch = {"image": b["image"].double(), "input_ids": b["input_ids"], "attention_mask": b["attention_mask"]}
+        loss = ref(batch)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+        print(f"step {k}: loss {loss.item():.10f}")
+    sums = {f"sum.{k}": v.double().sum().item() for k, v in sd0.items() if v.is_floating_point()}
+    npz("train_curve.npz", keep64=("losses",) + tuple(sums), losses=losses, **sums)
+
+
 def main():
     RCFG, RM, RC = import_reference()
+    if sys.argv[1:] == ["train_curve"]:
+        gen_train_curve(RC)
+        return
     gen_clip_loss(RC)
     gen_projection_head(RM)
     gen_masking()
     gen_patchify()
     gen_mae()
     gen_clip_model(RM, RC)
+    gen_train_curve(RC)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,8 @@ STEPS="${STEPS:-tests bench}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 480 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
+      rm -f gpurun_out/parity_${TAG}.jsonl
+      MAECLIP_PARITY_OUT=gpurun_out/parity_${TAG}.jsonl timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread \
         > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
       tail -3 gpurun_out/pytest_gpu_${TAG}.log ;;
     smoke)
@@ -28,6 +29,14 @@ for s in $STEPS; do
     gemmepi)
       GEMM_SET=epi timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/gemmepi_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gemmepi_${TAG}.jsonl; exit 1; }
       cat gpurun_out/gemmepi_${TAG}.jsonl ;;
+    testk)   # a -k selection of the GPU tests ($TESTK)
+      MAECLIP_PARITY_OUT=gpurun_out/parity_${TAG}.jsonl timeout -k 10 400 python -u -m pytest tests -x -v -m gpu -k "$TESTK" --timeout 120 --timeout-method thread \
+        > gpurun_out/pytest_k_${TAG}.log 2>&1 || { tail -40 gpurun_out/pytest_k_${TAG}.log; exit 1; }
+      tail -3 gpurun_out/pytest_k_${TAG}.log ;;
+    cliploss)
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/cliploss_${TAG} -o run --output-format csv -- \
+        python tools/clip_loss_bench.py > gpurun_out/cliploss_${TAG}.jsonl 2> gpurun_out/cliploss_${TAG}.err || { tail -30 gpurun_out/cliploss_${TAG}.err; exit 1; }
+      cat gpurun_out/cliploss_${TAG}.jsonl ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
         python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
