@@ -308,13 +308,20 @@ int32_t maeclip_mask_ids(const maeclip_mask_args* args, void* stream);
 
 /* visible-patch rows for the patch-embed GEMM (timm PatchEmbed Conv2d(k=s=p)
  * as GEMM): out[(b*keep+j), c*p*p+ky*p+kx] = img[b,c,py*p+ky,px*p+kx] for
- * patch l = ids_shuffle[b,j] (identity if NULL); columns >= C*p*p zeroed. */
+ * patch l = ids_shuffle[b,j] (identity if NULL); columns >= C*p*p zeroed.
+ * Image source: fp32 NCHW img, or -- when img_u8 is set (img ignored) -- the
+ * decoded uint8 RGB HWC pixels [B][S][S][C] (C = 3) with albumentations
+ * Normalize(u8_mean, u8_std, u8_max_pixel) (dataset.py:49) and the HWC->CHW
+ * permute (dataset.py:34) applied in the gather: the fp32 image is never
+ * materialised (same floats as maeclip_image_normalize_u8 + the fp32 gather). */
 typedef struct {
   const float* img;
   const int32_t* ids_shuffle;
   void* out;
   int64_t ld_out;
   int32_t B, C, S, p, keep, dtype;
+  const uint8_t* img_u8;
+  float u8_mean[3], u8_std[3], u8_max_pixel;
 } maeclip_patch_args;
 int32_t maeclip_patch_gather(const maeclip_patch_args* args, void* stream);
 
@@ -406,7 +413,9 @@ int32_t maeclip_unshuffle_bwd_partial_rows(int32_t B);
 
 /* MAE reconstruction loss (modeling_vit_mae.py:706-745 patchify, :852-859).
  * pred: decoder output rows [B, 1+L, ldp] (row 0 = cls, ignored); targets are
- * patchified from img on the fly (only for masked patches). fwd: row_loss [B*L]
+ * patchified from img on the fly (only for masked patches) -- fp32 NCHW img,
+ * or the uint8 HWC pixels img_u8 normalised in-kernel exactly as in
+ * maeclip_patch_args (u8_mean / u8_std / u8_max_pixel). fwd: row_loss [B*L]
  * = mask * mean_k diff^2 (sum / mask_count outside). bwd: dpred [B, 1+L, lddp]
  * = grad_out[0] * loss_scale * 2 diff mask / (P * mask_count) (columns
  * [P, lddp) zeroed); colsum_partial [maeclip_mae_loss_bwd_partial_rows(B, L)][P]
@@ -423,6 +432,8 @@ typedef struct {
   float* colsum_partial;
   float loss_scale, mask_count;
   int32_t B, C, S, p, L, norm_pix, dtype;
+  const uint8_t* img_u8;
+  float u8_mean[3], u8_std[3], u8_max_pixel;
 } maeclip_mae_loss_args;
 int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* args, void* stream);
 int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* args, void* stream);

@@ -25,7 +25,7 @@ from . import config as CFG
 from . import functions as Fn
 from . import kernels as K
 from .modules import (ImageEncoder, TextEncoder, ProjectionHead, MAEDecoder, WeightCache, compute_dtype,
-                      run_stack, _require_device)
+                      run_stack, _require_device, as_model_image)
 
 
 class CLIPModel(nn.Module):
@@ -90,6 +90,10 @@ class CLIPModel(nn.Module):
         return ids_shuffle, ids_restore, mask, keep
 
     def forward(self, batch):
+        """batch["image"]: the reference's fp32 NCHW normalised images
+        (dataset.py:44-58, :34), or the decoded uint8 RGB HWC pixels
+        [B, S, S, 3] -- then A.Normalize and the permute run inside the patch
+        gather and the MAE target read (data.py)."""
         img = batch["image"]
         _require_device(img, "image batch")
         dtype = compute_dtype(self.precision)
@@ -155,7 +159,7 @@ class CLIPModel(nn.Module):
             hspec = Fn.MaeHeadSpec(p=vit.patch_embed.patch_size, norm_pix=self.norm_pix_loss,
                                    mask_count=float(B * (L - keep)), loss_scale=1.0 / world, dtype=dtype,
                                    w_T=wp_T, b_pad=bp_pad)
-            ml = Fn.MaeHeadLossFn.apply(xd, img if img.dtype == torch.float32 else img.float(), mask, hspec,
+            ml = Fn.MaeHeadLossFn.apply(xd, as_model_image(img, vit.patch_embed.img_size), mask, hspec,
                                         dec.decoder_norm.weight, dec.decoder_norm.bias, dec.decoder_pred.weight,
                                         dec.decoder_pred.bias)
             self.last_losses["mae"] = ml.detach()

@@ -75,9 +75,12 @@ class MaskArgs(C.Structure):
                 ("seed", c_u64), ("step", c_u64), ("sample_offset", c_u64), ("step_ptr", c_vp)]
 
 
+_U8_FIELDS = [("img_u8", c_vp), ("u8_mean", c_f32 * 3), ("u8_std", c_f32 * 3), ("u8_max_pixel", c_f32)]
+
+
 class PatchArgs(C.Structure):
     _fields_ = [("img", c_vp), ("ids_shuffle", c_vp), ("out", c_vp), ("ld_out", c_i64),
-                ("B", c_i32), ("C", c_i32), ("S", c_i32), ("p", c_i32), ("keep", c_i32), ("dtype", c_i32)]
+                ("B", c_i32), ("C", c_i32), ("S", c_i32), ("p", c_i32), ("keep", c_i32), ("dtype", c_i32)] + _U8_FIELDS
 
 
 class TokensArgs(C.Structure):
@@ -98,7 +101,7 @@ class MaeLossArgs(C.Structure):
                 ("dpred", c_vp), ("lddp", c_i64), ("grad_out", c_vp), ("colsum_partial", c_vp),
                 ("loss_scale", c_f32), ("mask_count", c_f32),
                 ("B", c_i32), ("C", c_i32), ("S", c_i32), ("p", c_i32), ("L", c_i32), ("norm_pix", c_i32),
-                ("dtype", c_i32)]
+                ("dtype", c_i32)] + _U8_FIELDS
 
 
 class ClipArgs(C.Structure):

@@ -203,3 +203,27 @@ __host__ __device__ __forceinline__ uint32_t mc_hash4(uint64_t seed, uint64_t a,
   h = mc_mix64(h ^ c);
   return (uint32_t)(h >> 32);
 }
+
+// albumentations Normalize(mean, std, max_pixel_value) (dataset.py:49) as fp32
+// constants: m = f32(mean) * max_pixel, d = 1 / (f32(std) * max_pixel) (IEEE
+// fp32 product then reciprocal, on the host); a pixel x maps to
+// __fmul_rn(f32(x) - m, d) -- two roundings, no FMA. Shared by the input
+// pipeline (input.hip) and the kernels that read uint8 HWC pixels directly
+// (patch gather, MAE targets in mae.hip), so both routes give identical floats.
+struct NormConst {
+  float m[3], d[3];
+};
+// returns false on a non-positive std / max_pixel
+inline bool mc_norm_const(const float* mean, const float* stdv, float max_pixel, NormConst& k) {
+  if (!(max_pixel > 0.f)) return false;
+  for (int c = 0; c < 3; ++c) {
+    if (!(stdv[c] > 0.f)) return false;
+    k.m[c] = mean[c] * max_pixel;
+    const volatile float sd = stdv[c] * max_pixel;
+    k.d[c] = 1.0f / sd;
+  }
+  return true;
+}
+__device__ __forceinline__ float mc_norm_px(unsigned x, const NormConst& k, int c) {
+  return __fmul_rn((float)x - k.m[c], k.d[c]);
+}

@@ -22,10 +22,6 @@
 namespace {
 constexpr int NTH = 256;
 
-struct NormConst {
-  float m[3], d[3];
-};
-
 // 4 consecutive pixels of one row per thread: three 4-B loads of interleaved
 // RGB, one 16-B store per plane (W % 4 == 0)
 __global__ void __launch_bounds__(NTH) normalize_u8_x4_kernel(const uint8_t* __restrict__ src, float* __restrict__ dst,
@@ -44,8 +40,7 @@ __global__ void __launch_bounds__(NTH) normalize_u8_x4_kernel(const uint8_t* __r
     v4f o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float x = (float)v[3 * j + c] - k.m[c];
-      o[j] = __fmul_rn(x, k.d[c]);
+      o[j] = mc_norm_px(v[3 * j + c], k, c);
     }
     *(v4f*)(dst + (b * 3 + c) * HW + off) = o;
   }
@@ -58,8 +53,7 @@ __global__ void __launch_bounds__(NTH) normalize_u8_kernel(const uint8_t* __rest
   const int64_t b = pix / HW, off = pix % HW;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float x = (float)src[pix * 3 + c] - k.m[c];
-    dst[(b * 3 + c) * HW + off] = __fmul_rn(x, k.d[c]);
+    dst[(b * 3 + c) * HW + off] = mc_norm_px(src[pix * 3 + c], k, c);
   }
 }
 // OpenCV INTER_LINEAR source index / fixed-point weights of output coordinate d
@@ -119,21 +113,16 @@ __global__ void __launch_bounds__(NTH) preprocess_u8_kernel(const maeclip_image_
   }
   const int64_t plane = (int64_t)S * S;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) dst[((int64_t)b * 3 + c) * plane + p] = __fmul_rn((float)v[c] - k.m[c], k.d[c]);
+  for (int c = 0; c < 3; ++c) dst[((int64_t)b * 3 + c) * plane + p] = mc_norm_px(v[c], k, c);
 }
 }  // namespace
 
 extern "C" int32_t maeclip_image_preprocess_u8(const maeclip_preprocess_args* a, void* stream) {
   MC_CHECK_ARG(a && a->images && a->dst, "maeclip_image_preprocess_u8: null pointer");
   MC_CHECK_ARG(a->B >= 0 && a->S > 0 && a->S <= 8192 && a->B <= 65535, "maeclip_image_preprocess_u8: bad sizes");
-  MC_CHECK_ARG(a->max_pixel > 0.f, "maeclip_image_preprocess_u8: max_pixel must be > 0");
   NormConst k;
-  for (int c = 0; c < 3; ++c) {
-    MC_CHECK_ARG(a->std[c] > 0.f, "maeclip_image_preprocess_u8: std must be > 0");
-    k.m[c] = a->mean[c] * a->max_pixel;
-    const volatile float sd = a->std[c] * a->max_pixel;
-    k.d[c] = 1.0f / sd;
-  }
+  MC_CHECK_ARG(mc_norm_const(a->mean, a->std, a->max_pixel, k),
+               "maeclip_image_preprocess_u8: std and max_pixel must be > 0");
   if (a->B == 0) return 0;
   const int S = (int)a->S;
   hipLaunchKernelGGL(preprocess_u8_kernel, dim3((unsigned)((S * S + NTH - 1) / NTH), (unsigned)a->B), dim3(NTH), 0,
@@ -145,14 +134,9 @@ extern "C" int32_t maeclip_image_preprocess_u8(const maeclip_preprocess_args* a,
 extern "C" int32_t maeclip_image_normalize_u8(const maeclip_image_u8_args* a, void* stream) {
   MC_CHECK_ARG(a && a->src && a->dst, "maeclip_image_normalize_u8: null pointer");
   MC_CHECK_ARG(a->B >= 0 && a->H > 0 && a->W > 0, "maeclip_image_normalize_u8: bad sizes");
-  MC_CHECK_ARG(a->max_pixel > 0.f, "maeclip_image_normalize_u8: max_pixel must be > 0");
   NormConst k;
-  for (int c = 0; c < 3; ++c) {
-    MC_CHECK_ARG(a->std[c] > 0.f, "maeclip_image_normalize_u8: std must be > 0");
-    k.m[c] = a->mean[c] * a->max_pixel;
-    const volatile float sd = a->std[c] * a->max_pixel;   // fp32 product, then IEEE fp32 reciprocal
-    k.d[c] = 1.0f / sd;
-  }
+  MC_CHECK_ARG(mc_norm_const(a->mean, a->std, a->max_pixel, k),
+               "maeclip_image_normalize_u8: std and max_pixel must be > 0");
   const int64_t HW = a->H * a->W, npix = a->B * HW;
   if (npix == 0) return 0;
   hipStream_t s = (hipStream_t)stream;

@@ -89,6 +89,48 @@ __global__ void __launch_bounds__(NTH) patch_gather_kernel(const maeclip_patch_a
   }
 }
 
+// patch rows of the visible patches from the decoded uint8 HWC pixels, with
+// A.Normalize + the HWC->CHW permute (dataset.py:49, :34) folded in: one
+// thread per (row, ky) reads the p*C contiguous bytes of that patch row
+// (p = 16, C = 3: three 16-B loads) and writes the C channel runs of p values
+// (c, ky, kx order) -- 1 B read per 2 B (bf16) written instead of the fp32
+// image's 4 B read
+template <typename OT, bool VEC>
+__global__ void __launch_bounds__(NTH) patch_gather_u8_kernel(const maeclip_patch_args a, NormConst k) {
+  const int64_t seg = (int64_t)blockIdx.x * NTH + threadIdx.x;  // (row, ky)
+  const int p = a.p, C = a.C, S = a.S, w = S / p, L = w * w;
+  if (seg >= (int64_t)a.B * a.keep * p) return;
+  const int ky = (int)(seg % p);
+  const int64_t row = seg / p;
+  const int b = (int)(row / a.keep), j = (int)(row % a.keep);
+  const int l = a.ids_shuffle ? a.ids_shuffle[(int64_t)b * L + j] : j;
+  const int py = l / w, px = l % w;
+  const uint8_t* src = a.img_u8 + (((int64_t)b * S + py * p + ky) * S + (int64_t)px * p) * C;
+  OT* dst = (OT*)a.out + row * a.ld_out + ky * p;
+  if constexpr (VEC) {   // p = 16, C = 3: 48 bytes, 16-B aligned
+    const v4u q0 = *(const v4u*)src, q1 = *(const v4u*)(src + 16), q2 = *(const v4u*)(src + 32);
+    const unsigned wd[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v4f o[4];
+#pragma unroll
+      for (int kx = 0; kx < 16; ++kx) {
+        const int byte = kx * 3 + c;
+        o[kx >> 2][kx & 3] = mc_norm_px((wd[byte >> 2] >> (8 * (byte & 3))) & 0xffu, k, c);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st4<OT>(dst + c * 256 + 4 * q, o[q]);
+    }
+  } else {
+    for (int c = 0; c < C; ++c)
+      for (int kx = 0; kx < p; ++kx) st_from_f<OT>(dst + (int64_t)c * p * p + kx, mc_norm_px(src[kx * C + c], k, c));
+  }
+  if (ky == 0) {
+    OT* prow = (OT*)a.out + row * a.ld_out;
+    for (int64_t kk = (int64_t)C * p * p; kk < a.ld_out; ++kk) st_from_f<OT>(prow + kk, 0.f);
+  }
+}
+
 // x[b,0] = cls + pos[0]; x[b,1+j] = Y[b*keep+j] + pos[1+ids_shuffle[b,j]]   (f32 out)
 template <typename YT>
 __global__ void __launch_bounds__(NTH) tokens_fwd_kernel(const maeclip_tokens_args a) {
@@ -277,6 +319,37 @@ __device__ __forceinline__ void load_target(const maeclip_mae_loss_args& a, int 
   }
 }
 
+// The same target row from the uint8 HWC pixels: HF's patchify order
+// (ky, kx, c) IS the HWC byte order, so patch row ky is p*C contiguous bytes
+// of image row py*p + ky, copied to tg[ky*p*C ..] normalised (A.Normalize,
+// dataset.py:49; channel c = byte index mod C). VB = 16: 16-B loads (p*C and
+// S*C multiples of 16), else bytes.
+template <int VB>
+__device__ __forceinline__ void load_target_u8(const maeclip_mae_loss_args& a, const NormConst& k, int b, int l,
+                                               float* tg, int lane) {
+  const int C = a.C, p = a.p, w = a.S / p, R = p * C;
+  const int py = l / w, px = l % w;
+  const uint8_t* img = a.img_u8 + (((int64_t)b * a.S + py * p) * a.S + (int64_t)px * p) * C;
+  const int64_t rs = (int64_t)a.S * C;
+  if constexpr (VB == 16) {
+    const int vpr = R / 16;
+    for (int v = lane; v < p * vpr; v += 64) {
+      const int ky = v / vpr, off = (v - ky * vpr) * 16;
+      const v4u q = *(const v4u*)(img + ky * rs + off);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kk = off + e;
+        tg[ky * R + kk] = mc_norm_px((q[e >> 2] >> (8 * (e & 3))) & 0xffu, k, kk % C);
+      }
+    }
+  } else {
+    for (int v = lane; v < p * R; v += 64) {
+      const int ky = v / R, kk = v - ky * R;
+      tg[v] = mc_norm_px(img[ky * rs + kk], k, kk % C);
+    }
+  }
+}
+
 // norm_pix_loss: targets -> (t - mean) / sqrt(var + 1e-6), unbiased var (HF)
 __device__ __forceinline__ void norm_target(float* tg, int P, int lane) {
   float s = 0.f;
@@ -291,9 +364,13 @@ __device__ __forceinline__ void norm_target(float* tg, int P, int lane) {
   for (int k = lane; k < P; k += 64) tg[k] = (tg[k] - mean) * inv;
 }
 
+// VW > 0: fp32 NCHW image, VW floats per load; VW < 0: uint8 HWC pixels,
+// -VW bytes per load
 template <int VW>
-__device__ __forceinline__ void load_target_any(const maeclip_mae_loss_args& a, int b, int l, float* tg, int lane) {
-  load_target<VW>(a, b, l, tg, lane);
+__device__ __forceinline__ void load_target_any(const maeclip_mae_loss_args& a, const NormConst& k, int b, int l,
+                                                float* tg, int lane) {
+  if constexpr (VW > 0) load_target<VW>(a, b, l, tg, lane);
+  else load_target_u8<-VW>(a, k, b, l, tg, lane);
   if (a.norm_pix) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -307,7 +384,7 @@ __device__ __forceinline__ void load_target_any(const maeclip_mae_loss_args& a, 
 
 // One wave per patch (b, l); only masked patches (mask 1) read anything.
 template <typename PT, int VW>
-__global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_loss_args a) {
+__global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_loss_args a, NormConst nk) {
   __shared__ float tgs[NTH / 64][PMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t wid = (int64_t)blockIdx.x * (NTH / 64) + wave;
@@ -320,7 +397,7 @@ __global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_los
   const int b = (int)(wid / a.L), l = (int)(wid % a.L);
   const int P = a.C * a.p * a.p;
   float* tg = tgs[wave];
-  load_target_any<VW>(a, b, l, tg, lane);
+  load_target_any<VW>(a, nk, b, l, tg, lane);
   const PT* pred = (const PT*)a.pred + ((int64_t)b * (a.L + 1) + 1 + l) * a.ldp;
   float s = 0.f;
   for (int k = 4 * lane; k < P; k += 256) {
@@ -339,7 +416,7 @@ __global__ void __launch_bounds__(NTH) mae_loss_fwd_kernel(const maeclip_mae_los
 // (decoder_pred bias gradient) -> colsum_partial[b * nchunk + chunk][P].
 constexpr int RB = 16;
 template <typename PT, int VW>
-__global__ void __launch_bounds__(NTH) mae_loss_bwd_kernel(const maeclip_mae_loss_args a) {
+__global__ void __launch_bounds__(NTH) mae_loss_bwd_kernel(const maeclip_mae_loss_args a, NormConst nk) {
   __shared__ float tgs[NTH / 64][PMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.x, chunk = blockIdx.y;
@@ -359,7 +436,7 @@ __global__ void __launch_bounds__(NTH) mae_loss_bwd_kernel(const maeclip_mae_los
       continue;
     }
     const PT* prow = (const PT*)a.pred + ((int64_t)b * (a.L + 1) + r) * a.ldp;
-    load_target_any<VW>(a, b, r - 1, tg, lane);
+    load_target_any<VW>(a, nk, b, r - 1, tg, lane);
     const float g = gscale * mk;
 #pragma unroll
     for (int i = 0; i < PMAX / 256; ++i) {
@@ -399,9 +476,28 @@ extern "C" int32_t maeclip_mask_ids(const maeclip_mask_args* a, void* stream) {
 }
 
 extern "C" int32_t maeclip_patch_gather(const maeclip_patch_args* a, void* stream) {
-  MC_CHECK_ARG(a && a->img && a->out, "maeclip_patch_gather: null pointer");
+  MC_CHECK_ARG(a && (a->img || a->img_u8) && a->out, "maeclip_patch_gather: null pointer");
   MC_CHECK_ARG(a->p > 0 && a->S % a->p == 0 && a->keep > 0 && a->ld_out >= (int64_t)a->C * a->p * a->p,
                "maeclip_patch_gather: bad sizes");
+  if (a->img_u8) {
+    NormConst k;
+    MC_CHECK_ARG(a->C == 3, "maeclip_patch_gather: uint8 pixels need C == 3 (RGB)");
+    MC_CHECK_ARG(mc_norm_const(a->u8_mean, a->u8_std, a->u8_max_pixel, k),
+                 "maeclip_patch_gather: u8_std and u8_max_pixel must be > 0");
+    const int64_t nseg = (int64_t)a->B * a->keep * a->p;
+    dim3 grid((unsigned)((nseg + NTH - 1) / NTH));
+    const bool vec = a->p == 16 && ((uintptr_t)a->img_u8 & 15) == 0 && (a->S * 3) % 16 == 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (a->dtype == MAECLIP_BF16) {
+      if (vec) hipLaunchKernelGGL((patch_gather_u8_kernel<bf16_t, true>), grid, dim3(NTH), 0, st, *a, k);
+      else hipLaunchKernelGGL((patch_gather_u8_kernel<bf16_t, false>), grid, dim3(NTH), 0, st, *a, k);
+    } else {
+      if (vec) hipLaunchKernelGGL((patch_gather_u8_kernel<float, true>), grid, dim3(NTH), 0, st, *a, k);
+      else hipLaunchKernelGGL((patch_gather_u8_kernel<float, false>), grid, dim3(NTH), 0, st, *a, k);
+    }
+    MC_CHECK_LAUNCH("maeclip_patch_gather(u8)");
+    return 0;
+  }
   const int64_t nseg = (int64_t)a->B * a->keep * a->C * a->p;
   dim3 grid((unsigned)((nseg + NTH - 1) / NTH));
   if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((patch_gather_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
@@ -460,17 +556,32 @@ extern "C" int32_t maeclip_unshuffle_bwd(const maeclip_unshuffle_args* a, void* 
 extern "C" int32_t maeclip_unshuffle_bwd_partial_rows(int32_t B) { return B * UQ; }
 
 namespace {
-int check_loss(const maeclip_mae_loss_args* a, bool bwd) {
-  MC_CHECK_ARG(a && a->pred && a->img && a->mask, "maeclip_mae_loss: null pointer");
+int check_loss(const maeclip_mae_loss_args* a, bool bwd, NormConst& k) {
+  MC_CHECK_ARG(a && a->pred && (a->img || a->img_u8) && a->mask, "maeclip_mae_loss: null pointer");
   const int P = a->C * a->p * a->p;
   MC_CHECK_ARG(P <= PMAX && P % 4 == 0 && a->ldp % 4 == 0 && a->ldp >= P && a->S % a->p == 0,
                "maeclip_mae_loss: p*p*C must be a multiple of 4, <= %d", PMAX);
-  MC_CHECK_ARG(((uintptr_t)a->img & 15) == 0 && ((uintptr_t)a->pred & 7) == 0 && a->S % 4 == 0,
-               "maeclip_mae_loss: misaligned image / pred");
+  if (a->img_u8) {
+    MC_CHECK_ARG(a->C == 3, "maeclip_mae_loss: uint8 pixels need C == 3 (RGB)");
+    MC_CHECK_ARG(mc_norm_const(a->u8_mean, a->u8_std, a->u8_max_pixel, k),
+                 "maeclip_mae_loss: u8_std and u8_max_pixel must be > 0");
+  } else {
+    k = NormConst{};
+    MC_CHECK_ARG(((uintptr_t)a->img & 15) == 0 && a->S % 4 == 0, "maeclip_mae_loss: misaligned image");
+  }
+  MC_CHECK_ARG(((uintptr_t)a->pred & 7) == 0, "maeclip_mae_loss: misaligned pred");
   if (bwd) MC_CHECK_ARG(a->dpred && a->lddp % 4 == 0 && a->lddp >= P && a->mask_count > 0.f,
                         "maeclip_mae_loss_bwd: bad dpred / mask_count");
   else MC_CHECK_ARG(a->row_loss != nullptr, "maeclip_mae_loss_fwd: null row_loss");
   return 0;
+}
+
+// load width of the target read: fp32 NCHW floats (4 / 2 / 1) or, for uint8
+// HWC pixels, 16-B vectors (-16) when every patch row is 16-B aligned, else bytes (-1)
+int loss_vw(const maeclip_mae_loss_args& a) {
+  if (a.img_u8)
+    return ((a.p * a.C) % 16 == 0 && ((int64_t)a.S * a.C) % 16 == 0 && ((uintptr_t)a.img_u8 & 15) == 0) ? -16 : -1;
+  return a.p % 4 == 0 ? 4 : (a.p % 2 == 0 ? 2 : 1);
 }
 
 }  // namespace
@@ -478,16 +589,19 @@ int check_loss(const maeclip_mae_loss_args* a, bool bwd) {
 extern "C" int32_t maeclip_mae_loss_bwd_partial_rows(int32_t B, int32_t L) { return B * ((L + 1 + RB - 1) / RB); }
 
 extern "C" int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* a, void* stream) {
-  if (int e = check_loss(a, false)) return e;
+  NormConst k;
+  if (int e = check_loss(a, false, k)) return e;
   const int64_t nw = (int64_t)a->B * a->L;
   dim3 grid((unsigned)((nw + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-  const int vw = a->p % 4 == 0 ? 4 : (a->p % 2 == 0 ? 2 : 1);
-#define FWD(PT, VW) hipLaunchKernelGGL((mae_loss_fwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a)
+  const int vw = loss_vw(*a);
+#define FWD(PT, VW) hipLaunchKernelGGL((mae_loss_fwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a, k)
   if (a->dtype == MAECLIP_BF16) {
-    if (vw == 4) FWD(bf16_t, 4); else if (vw == 2) FWD(bf16_t, 2); else FWD(bf16_t, 1);
+    switch (vw) { case 4: FWD(bf16_t, 4); break; case 2: FWD(bf16_t, 2); break; case 1: FWD(bf16_t, 1); break;
+                  case -16: FWD(bf16_t, -16); break; default: FWD(bf16_t, -1); }
   } else {
-    if (vw == 4) FWD(float, 4); else if (vw == 2) FWD(float, 2); else FWD(float, 1);
+    switch (vw) { case 4: FWD(float, 4); break; case 2: FWD(float, 2); break; case 1: FWD(float, 1); break;
+                  case -16: FWD(float, -16); break; default: FWD(float, -1); }
   }
 #undef FWD
   MC_CHECK_LAUNCH("maeclip_mae_loss_fwd");
@@ -495,15 +609,18 @@ extern "C" int32_t maeclip_mae_loss_fwd(const maeclip_mae_loss_args* a, void* st
 }
 
 extern "C" int32_t maeclip_mae_loss_bwd(const maeclip_mae_loss_args* a, void* stream) {
-  if (int e = check_loss(a, true)) return e;
+  NormConst k;
+  if (int e = check_loss(a, true, k)) return e;
   dim3 grid((unsigned)a->B, (unsigned)((a->L + 1 + RB - 1) / RB));
   hipStream_t s = (hipStream_t)stream;
-  const int vw = a->p % 4 == 0 ? 4 : (a->p % 2 == 0 ? 2 : 1);
-#define BWD(PT, VW) hipLaunchKernelGGL((mae_loss_bwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a)
+  const int vw = loss_vw(*a);
+#define BWD(PT, VW) hipLaunchKernelGGL((mae_loss_bwd_kernel<PT, VW>), grid, dim3(NTH), 0, s, *a, k)
   if (a->dtype == MAECLIP_BF16) {
-    if (vw == 4) BWD(bf16_t, 4); else if (vw == 2) BWD(bf16_t, 2); else BWD(bf16_t, 1);
+    switch (vw) { case 4: BWD(bf16_t, 4); break; case 2: BWD(bf16_t, 2); break; case 1: BWD(bf16_t, 1); break;
+                  case -16: BWD(bf16_t, -16); break; default: BWD(bf16_t, -1); }
   } else {
-    if (vw == 4) BWD(float, 4); else if (vw == 2) BWD(float, 2); else BWD(float, 1);
+    switch (vw) { case 4: BWD(float, 4); break; case 2: BWD(float, 2); break; case 1: BWD(float, 1); break;
+                  case -16: BWD(float, -16); break; default: BWD(float, -1); }
   }
 #undef BWD
   MC_CHECK_LAUNCH("maeclip_mae_loss_bwd");

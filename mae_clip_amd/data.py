@@ -21,8 +21,7 @@ from . import _lib as L
 from .kernels import _dev, _call, _stream
 
 # ImageNet statistics of albumentations' A.Normalize defaults (dataset.py:49)
-IMAGENET_MEAN = (0.485, 0.456, 0.406)
-IMAGENET_STD = (0.229, 0.224, 0.225)
+from .kernels import IMAGENET_MEAN, IMAGENET_STD  # noqa: E402
 
 
 def normalize_u8(images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, max_pixel_value=255.0,

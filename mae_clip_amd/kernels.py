@@ -403,12 +403,39 @@ def mask_ids(B, L_, len_keep, seed, step, sample_offset, device, want_noise=Fals
     return ids_shuffle, ids_restore, mask, noise
 
 
+# albumentations A.Normalize defaults of the reference's transforms (dataset.py:49)
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def is_u8_image(img):
+    """uint8 [B, S, S, 3] decoded RGB pixels (HWC), normalised inside the kernels."""
+    return img.dtype == torch.uint8 and img.dim() == 4 and img.shape[-1] == 3
+
+
+def image_geometry(img):
+    """(B, C, S) of an fp32 NCHW batch or a uint8 HWC pixel batch."""
+    if is_u8_image(img):
+        return img.shape[0], 3, img.shape[1]
+    return img.shape[0], img.shape[1], img.shape[2]
+
+
+def _u8_fields(img):
+    """img_u8 / Normalize constants of the ABI structs (img: NCHW fp32 -> unset)."""
+    if not is_u8_image(img):
+        return dict(img=img.data_ptr())
+    return dict(img=None, img_u8=img.data_ptr(), u8_mean=(C.c_float * 3)(*IMAGENET_MEAN),
+                u8_std=(C.c_float * 3)(*IMAGENET_STD), u8_max_pixel=255.0)
+
+
 def patch_gather(img, ids_shuffle, keep, p, kpad, dtype):
+    """Visible-patch rows for the patch-embed GEMM from an fp32 NCHW image or
+    from uint8 HWC pixels (A.Normalize + permute fused, dataset.py:49, :34)."""
     _dev(img, ids_shuffle)
-    B, Cc, S, _ = img.shape
+    B, Cc, S = image_geometry(img)
     out = torch.empty((B * keep, kpad), device=img.device, dtype=dtype)
-    a = L.PatchArgs(img=img.data_ptr(), ids_shuffle=_ptr(ids_shuffle), out=out.data_ptr(), ld_out=kpad, B=B, C=Cc, S=S,
-                    p=p, keep=keep, dtype=_dt(out))
+    a = L.PatchArgs(ids_shuffle=_ptr(ids_shuffle), out=out.data_ptr(), ld_out=kpad, B=B, C=Cc, S=S,
+                    p=p, keep=keep, dtype=_dt(out), **_u8_fields(img))
     _call("maeclip_patch_gather", C.byref(a), _stream())
     return out
 
@@ -463,19 +490,19 @@ def unshuffle_bwd(dout, ids_restore, B, L_, keep, dy_dtype):
 
 
 def mae_loss_fwd(pred, img, mask, p, norm_pix):
-    B, Cc, S, _ = img.shape
+    B, Cc, S = image_geometry(img)
     L_ = mask.shape[1]
     row = torch.empty((B * L_,), device=img.device, dtype=torch.float32)
-    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
+    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), mask=mask.data_ptr(),
                       row_loss=row.data_ptr(), dpred=None, lddp=0, grad_out=None, colsum_partial=None,
                       loss_scale=1.0, mask_count=1.0, B=B, C=Cc, S=S, p=p, L=L_, norm_pix=int(norm_pix),
-                      dtype=_dt(pred))
+                      dtype=_dt(pred), **_u8_fields(img))
     _call("maeclip_mae_loss_fwd", C.byref(a), _stream())
     return row
 
 
 def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=1.0):
-    B, Cc, S, _ = img.shape
+    B, Cc, S = image_geometry(img)
     L_ = mask.shape[1]
     P = Cc * p * p
     # padded pred rows (decoder_pred N rounded up for the GEMM): the kernel
@@ -483,10 +510,10 @@ def mae_loss_bwd(pred, img, mask, p, norm_pix, grad_out, mask_count, loss_scale=
     dpred = torch.empty_like(pred)
     G = int(L.lib().maeclip_mae_loss_bwd_partial_rows(B, L_))
     cs = torch.empty((G, P), device=img.device, dtype=torch.float32)
-    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), img=img.data_ptr(), mask=mask.data_ptr(),
+    a = L.MaeLossArgs(pred=pred.data_ptr(), ldp=pred.stride(0), mask=mask.data_ptr(),
                       row_loss=None, dpred=dpred.data_ptr(), lddp=dpred.stride(0), grad_out=_ptr(grad_out),
                       colsum_partial=cs.data_ptr(), loss_scale=loss_scale, mask_count=float(mask_count),
-                      B=B, C=Cc, S=S, p=p, L=L_, norm_pix=int(norm_pix), dtype=_dt(pred))
+                      B=B, C=Cc, S=S, p=p, L=L_, norm_pix=int(norm_pix), dtype=_dt(pred), **_u8_fields(img))
     _call("maeclip_mae_loss_bwd", C.byref(a), _stream())
     return dpred, cs
 

@@ -50,6 +50,21 @@ def _require_device(t: torch.Tensor, what: str):
                            "move the model and batch to 'cuda'")
 
 
+def as_model_image(img, size):
+    """Validate an image batch: fp32 NCHW [B,3,S,S] (other float dtypes are
+    cast) or uint8 HWC pixels [B,S,S,3] (kept as they are: the kernels read
+    the pixels and apply A.Normalize themselves). Returns a contiguous tensor."""
+    if K.is_u8_image(img):
+        if img.shape[1] != size or img.shape[2] != size:
+            raise ValueError(f"uint8 pixel batch must be [B,{size},{size},3], got {tuple(img.shape)}")
+        return img.contiguous()
+    if img.dim() != 4 or img.shape[1] != 3 or img.shape[2] != size or img.shape[3] != size:
+        raise ValueError(f"image batch must be [B,3,{size},{size}] (fp32) or [B,{size},{size},3] (uint8), "
+                         f"got {tuple(img.shape)}")
+    img = img if img.dtype == torch.float32 else img.float()
+    return img.contiguous()
+
+
 def _trunc_normal_(t, std=0.02):
     nn.init.trunc_normal_(t, std=std, a=-2 * std, b=2 * std)
 
@@ -236,15 +251,15 @@ class VisionTransformer(nn.Module):
                 cache.register_fp8(p)
 
     def forward_tokens(self, img, dtype, cache, ids_shuffle=None, ids_restore=None, keep=None, world=1):
+        """img: the reference's fp32 NCHW batch [B,3,S,S] (dataset.py:34), or the
+        decoded uint8 RGB pixels [B,S,S,3] (HWC), normalised inside the patch
+        gather (A.Normalize of dataset.py:49 fused; no fp32 image in HBM)."""
         _require_device(img, "image batch")
-        B, C, S, S2 = img.shape
+        img = as_model_image(img, self.patch_embed.img_size)
         pe = self.patch_embed
-        if S != pe.img_size or S2 != pe.img_size or C != 3:
-            raise ValueError(f"image batch must be [B,3,{pe.img_size},{pe.img_size}], got {tuple(img.shape)}")
+        B = img.shape[0]
         L = pe.num_patches
         keep = L if keep is None else keep
-        img = img if img.dtype == torch.float32 else img.float()
-        img = img.contiguous()
         w = pe.proj.weight
         kreal = w[0].numel()
         epc = 8 if dtype == torch.bfloat16 else 4

@@ -630,3 +630,33 @@ def test_attention_deterministic(dev, shape):
     for r in runs[1:]:
         for x, y in zip(r, runs[0]):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(6, 224, 16, 49), (3, 336, 14, 144), (4, 32, 8, 4), (2, 224, 16, 196)])
+def test_uint8_pixels_fused_into_gather_and_mae_targets(dev, dtype, geo):
+    """A.Normalize + permute (dataset.py:49, :34) folded
+    into the patch gather and the MAE target read. Reading the uint8 HWC pixels
+    directly must give the SAME bits as normalize_u8 (the materialised fp32
+    NCHW image, itself bit-exact vs the numpy restatement) + the fp32 kernels:
+    gathered rows, per-patch losses (norm_pix off / on) and dpred."""
+    from mae_clip_amd.data import normalize_u8
+    B, S, p, keep = geo
+    L_ = (S // p) ** 2
+    g = torch.Generator().manual_seed(71)
+    px = torch.randint(0, 256, (B, S, S, 3), generator=g, dtype=torch.uint8).to(dev)
+    img = normalize_u8(px)
+    ids_s, _, mask, _ = K.mask_ids(B, L_, keep, seed=2, step=5, sample_offset=0, device=dev)
+    kpad = (3 * p * p + 63) // 64 * 64
+    a = K.patch_gather(px, ids_s, keep, p, kpad, dtype)
+    b = K.patch_gather(img, ids_s, keep, p, kpad, dtype)
+    assert torch.equal(a, b)
+    P = 3 * p * p
+    ldp = (P + 63) // 64 * 64
+    pred = _rand((B * (L_ + 1), ldp), dtype, dev, seed=72)
+    gl = torch.tensor(0.3, device=dev)
+    for norm_pix in (False, True):
+        assert torch.equal(K.mae_loss_fwd(pred, px, mask, p, norm_pix), K.mae_loss_fwd(pred, img, mask, p, norm_pix))
+        d1, c1 = K.mae_loss_bwd(pred, px, mask, p, norm_pix, gl, float(mask.sum().item()))
+        d2, c2 = K.mae_loss_bwd(pred, img, mask, p, norm_pix, gl, float(mask.sum().item()))
+        assert torch.equal(d1, d2) and torch.equal(c1, c2)

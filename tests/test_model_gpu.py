@@ -494,3 +494,26 @@ def test_vitl14_336_full_depth_bf16_vs_oracle(dev):
     rel = abs(loss.item() - rloss) / max(1.0, abs(rloss))
     record_parity("vitl14_336_full_depth_bf16_vs_oracle", loss_rel=rel, product=loss.item(), oracle=rloss)
     assert rel < 2e-2, (loss.item(), rloss)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("mask_ratio", [0.75, 0.0])
+def test_uint8_pixel_batch_equals_normalised_batch(dev, precision, mask_ratio):
+    """CLIPModel.forward on the decoded uint8 RGB pixels [B, S, S, 3] (A.Normalize
+    + permute fused into the patch gather and the MAE target read) == the same
+    model on the fp32 NCHW batch normalize_u8 produces (dataset.py:44-58, :34):
+    identical loss and gradients, bit for bit."""
+    from mae_clip_amd.data import normalize_u8
+    g = torch.Generator().manual_seed(5)
+    px = torch.randint(0, 256, (8, 32, 32, 3), generator=g, dtype=torch.uint8).to(dev)
+    b = make_batch(8, 32)
+    out = []
+    for image in (px, normalize_u8(px)):
+        prod, _ = build_pair(precision, mask_ratio=mask_ratio)
+        prod.eval()
+        loss = prod({"image": image, "input_ids": b["input_ids"].to(dev), "attention_mask": b["attention_mask"].to(dev)})
+        loss.backward()
+        out.append((loss.detach(), {n: p.grad.clone() for n, p in prod.named_parameters() if p.requires_grad}))
+    assert torch.equal(out[0][0], out[1][0])
+    for n, gr in out[0][1].items():
+        assert torch.equal(gr, out[1][1][n]), n
