@@ -15,8 +15,9 @@ from . import _lib as L
 KC, RC = 0, 1
 EPI_NONE, EPI_GELU, EPI_RESID, EPI_DGELU, EPI_GELU_D, EPI_MUL_AUX = 0, 1, 2, 3, 4, 5
 
-# Optional instrumentation: LAUNCH_HOOK(key, flops, launch_fn) wraps every GEMM
-# launch (bench.py brackets them with HIP events on the current stream).
+# Optional instrumentation: LAUNCH_HOOK(key, flops, nbytes, launch_fn) wraps every
+# GEMM launch and every grouped weight-gradient launch (bench.py brackets them
+# with HIP events / timestamps on the current stream).
 LAUNCH_HOOK = None
 
 
@@ -264,7 +265,17 @@ def wgrad_grouped(items, beta=0.0):
     lib = L.lib()
     nb = int(lib.maeclip_wgrad_grouped_workspace(probs, n, M, dt))
     ws = torch.empty((max(nb, 4) // 4,), device=items[0][0].device, dtype=torch.float32) if nb > 0 else None
-    _call("maeclip_wgrad_grouped", probs, n, M, dt, beta, _ptr(ws), nb, _stream())
+    launch = lambda: _call("maeclip_wgrad_grouped", probs, n, M, dt, beta, _ptr(ws), nb, _stream())
+    if LAUNCH_HOOK is None:
+        launch()
+        return
+    es = items[0][0].element_size()
+    flops = sum(2.0 * M * dy.shape[1] * x.shape[1] for dy, x, _ in items)
+    # algorithmic bytes: dy and x once each, dW written (read too when beta != 0)
+    nbytes = sum(M * (dy.shape[1] + x.shape[1]) * es + dy.shape[1] * x.shape[1] * 4 * (2 if beta else 1)
+                 for dy, x, _ in items)
+    key = f"wgrad_grouped M{M} x{n} N{items[0][0].shape[1]} K{items[0][1].shape[1]} {'bf16' if dt == L.BF16 else 'f32'}>f32"
+    LAUNCH_HOOK(key, flops, nbytes, launch)
 
 
 # ------------------------------------------------------------- reductions

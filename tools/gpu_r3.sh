@@ -37,6 +37,10 @@ for s in $STEPS; do
       timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/cliploss_${TAG} -o run --output-format csv -- \
         python tools/clip_loss_bench.py > gpurun_out/cliploss_${TAG}.jsonl 2> gpurun_out/cliploss_${TAG}.err || { tail -30 gpurun_out/cliploss_${TAG}.err; exit 1; }
       cat gpurun_out/cliploss_${TAG}.jsonl ;;
+    hbprof)  # hipBLASLt kernel names / durations for the production shapes (calibration only)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/hbprof_${TAG} -o run --output-format csv -- \
+        python tools/gemm_bench.py > gpurun_out/hbprof_${TAG}.log 2>&1 || { tail -30 gpurun_out/hbprof_${TAG}.log; exit 1; }
+      tail -3 gpurun_out/hbprof_${TAG}.log ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
         python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
