@@ -288,6 +288,10 @@ int64_t maeclip_mt_chunk(void);
 /* dev_entries: device copy of host_entries (host pointer used for the grid size) */
 int32_t maeclip_cast_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries, int32_t ne,
                            void* stream);
+/* flat conversion dst[i] = scale * src[i], dtypes MAECLIP_F32 / MAECLIP_BF16
+ * (RNE): the bf16 gradient all-reduce buckets of data parallelism */
+int32_t maeclip_cast_flat(const void* src, int32_t src_dtype, void* dst, int32_t dst_dtype, int64_t n, float scale,
+                          void* stream);
 /* torch.optim.AdamW step (main.py:101-103,59) fused over all parameters */
 int32_t maeclip_adamw_multi(const maeclip_mt_entry* dev_entries, const maeclip_mt_entry* host_entries, int32_t ne,
                             const maeclip_adamw_hparams* hp, void* stream);

@@ -165,6 +165,7 @@ _SIGS = {
     "maeclip_rows_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),
     "maeclip_colsum_scratch": (c_i64, [c_i64, c_i64]),
+    "maeclip_cast_flat": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i64, c_f32, c_vp]),
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "maeclip_pool_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp]),
     "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp, c_vp]),

@@ -242,6 +242,19 @@ __global__ void __launch_bounds__(NTH) cast_multi_kernel(const maeclip_mt_entry*
   }
 }
 
+// flat dtype conversion dst = scale * src (f32 <-> bf16, RNE): the bf16
+// gradient all-reduce buckets of data parallelism (distributed.py)
+template <typename ST, typename DT>
+__global__ void __launch_bounds__(NTH) cast_flat_kernel(const ST* __restrict__ src, DT* __restrict__ dst, int64_t n,
+                                                        float scale) {
+  const int64_t i = ((int64_t)blockIdx.x * NTH + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    st4<DT>(dst + i, ld4<ST>(src + i) * scale);
+  } else {
+    for (int64_t j = i; j < n; ++j) st_from_f<DT>(dst + j, ld_as_f<ST>(src + j) * scale);
+  }
+}
+
 // torch.optim.AdamW (decoupled weight decay), torch/optim/adamw.py _single_tensor_adamw:
 //   p *= 1 - lr*wd ; m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
 //   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
@@ -428,5 +441,28 @@ extern "C" int32_t maeclip_memcpy_h2d(void* dst, const void* src, size_t bytes, 
     maeclip::set_error("maeclip_memcpy_h2d: %s", hipGetErrorString(e));
     return -2;
   }
+  return 0;
+}
+
+extern "C" int32_t maeclip_cast_flat(const void* src, int32_t src_dtype, void* dst, int32_t dst_dtype, int64_t n,
+                                     float scale, void* stream) {
+  MC_CHECK_ARG(src && dst && n >= 0, "maeclip_cast_flat: bad args");
+  MC_CHECK_ARG((src_dtype == MAECLIP_F32 || src_dtype == MAECLIP_BF16) &&
+                   (dst_dtype == MAECLIP_F32 || dst_dtype == MAECLIP_BF16),
+               "maeclip_cast_flat: dtypes must be f32 / bf16");
+  MC_CHECK_ARG(((uintptr_t)src & 7) == 0 && ((uintptr_t)dst & 7) == 0, "maeclip_cast_flat: 8-B aligned buffers");
+  if (n == 0) return 0;
+  dim3 grid((unsigned)((n + 4 * NTH - 1) / (4 * NTH)));
+  hipStream_t s = (hipStream_t)stream;
+  if (src_dtype == MAECLIP_F32 && dst_dtype == MAECLIP_BF16)
+    hipLaunchKernelGGL((cast_flat_kernel<float, bf16_t>), grid, dim3(NTH), 0, s, (const float*)src, (bf16_t*)dst, n, scale);
+  else if (src_dtype == MAECLIP_BF16 && dst_dtype == MAECLIP_F32)
+    hipLaunchKernelGGL((cast_flat_kernel<bf16_t, float>), grid, dim3(NTH), 0, s, (const bf16_t*)src, (float*)dst, n, scale);
+  else if (src_dtype == MAECLIP_F32)
+    hipLaunchKernelGGL((cast_flat_kernel<float, float>), grid, dim3(NTH), 0, s, (const float*)src, (float*)dst, n, scale);
+  else
+    hipLaunchKernelGGL((cast_flat_kernel<bf16_t, bf16_t>), grid, dim3(NTH), 0, s, (const bf16_t*)src, (bf16_t*)dst, n,
+                       scale);
+  MC_CHECK_LAUNCH("maeclip_cast_flat");
   return 0;
 }

@@ -659,6 +659,16 @@ class MultiTensorPlan:
         self.n = n
 
 
+def cast_flat(src, dst, scale=1.0):
+    """dst = scale * src elementwise (f32 <-> bf16, same numel, dense)."""
+    _dev(src, dst)
+    if src.numel() != dst.numel() or not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("cast_flat: dense tensors of equal size")
+    _call("maeclip_cast_flat", src.data_ptr(), _dt(src), dst.data_ptr(), _dt(dst), src.numel(), float(scale),
+          _stream())
+    return dst
+
+
 def cast_multi(plan: MultiTensorPlan):
     _call("maeclip_cast_multi", plan.dev.data_ptr(), plan.host, plan.n, _stream())
 

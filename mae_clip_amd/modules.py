@@ -184,6 +184,25 @@ class Block(nn.Module):
             nn.init.zeros_(lin.bias)
 
 
+def chunk_bounds(n, chunk):
+    """[c0, c1) block ranges of a stack in forward order. chunk: None (one
+    Function), an int (equal chunks), or a tuple of chunk sizes in forward
+    order whose last entry repeats (e.g. (2, 4, 6): blocks 0-1, 2-5, 6-11 --
+    the backward runs the top chunk first, so the bottom chunk, whose
+    all-reduce cannot overlap any later backward work, is the small one)."""
+    if not chunk:
+        return [(0, n)]
+    sizes = [chunk] if isinstance(chunk, int) else [int(c) for c in chunk]
+    if any(c <= 0 for c in sizes):
+        raise ValueError(f"chunk sizes must be positive: {chunk}")
+    out, c0, i = [], 0, 0
+    while c0 < n:
+        c1 = min(n, c0 + sizes[min(i, len(sizes) - 1)])
+        out.append((c0, c1))
+        c0, i = c1, i + 1
+    return out
+
+
 def run_stack(blocks, x, heads, dtype, cache: WeightCache, chunk=None, fp8=True):
     """The blocks as one TransformerStackFn, or as consecutive Functions of
     `chunk` blocks: autograd accumulates a Function's parameter gradients when
@@ -193,9 +212,8 @@ def run_stack(blocks, x, heads, dtype, cache: WeightCache, chunk=None, fp8=True)
     backward is otherwise fully exposed). fp8=False keeps a stack on bf16 GEMMs
     when the cache is in fp8 mode."""
     B, n, D = x.shape
-    chunk = chunk or len(blocks)
-    for c0 in range(0, len(blocks), chunk):
-        part = blocks[c0:c0 + chunk]
+    for c0, c1 in chunk_bounds(len(blocks), chunk):
+        part = blocks[c0:c1]
         wT = [tuple(cache.get(w, dtype) for w in blk.gemm_weights()) for blk in part]
         w8 = ([tuple(cache.get_fp8(w) for w in blk.gemm_weights()) for blk in part]
               if fp8 and getattr(cache, "fp8", False) and dtype == torch.bfloat16 else None)

@@ -90,14 +90,14 @@ def _dp_forward(m, cfg, batch, rank, world):
     return loss + cfg.mae_weight * ml / world, loss.detach(), ml.detach(), mask
 
 
-def _dp_body(bucket_mb, overlap, rank, world):
+def _dp_body(bucket_mb, overlap, rank, world, grad_dtype=torch.float32):
         from mae_clip_amd.distributed import DataParallel
         m, cfg, batch = _model_and_batch()
         if rank == 1:   # replicas start different; DataParallel broadcasts rank 0's weights
             with torch.no_grad():
                 for p in m.parameters():
                     p.add_(1.0)
-        dp = DataParallel(m, bucket_mb=bucket_mb)
+        dp = DataParallel(m, bucket_mb=bucket_mb, grad_dtype=grad_dtype)
         dp.overlap = overlap
         sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
         local = {k: v[sl] for k, v in batch.items()}
@@ -163,3 +163,22 @@ def test_data_parallel_rejects_ragged_batches():
     """ranks with different local B fail with a clear error, not a hang."""
     res = run_ranks(_ragged_body)
     assert all(r is not None and "different local batch sizes" in r for r in res)
+
+
+def test_data_parallel_bf16_gradient_allreduce():
+    """opt-in bf16 all-reduce buckets (DataParallel(grad_dtype=bfloat16)): every
+    gradient within 1e-2 relative L2 of the fp32 single-process full batch
+    (two bf16 roundings + one bf16 add per element), ranks identical."""
+    res = run_ranks(functools.partial(_dp_body, 0.05, True, grad_dtype=torch.bfloat16))
+    m, cfg, batch = _model_and_batch()
+    m(batch, step=0).backward()
+    worst = 0.0
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        g = res[0][3][n].double()
+        den = p.grad.double().norm().item()
+        if den > 0:
+            worst = max(worst, (g - p.grad.double()).norm().item() / den)
+        assert torch.equal(res[0][3][n], res[1][3][n]), n
+    assert worst < 1e-2, worst

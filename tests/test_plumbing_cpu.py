@@ -156,3 +156,12 @@ def test_data_parallel_arena_plumbing():
         adopted, nparams, nbuckets, owned = out[r]
         assert adopted == nparams, (adopted, nparams)
         assert nbuckets > 2 and owned
+
+
+def test_chunk_bounds():
+    from mae_clip_amd.modules import chunk_bounds
+    assert chunk_bounds(12, None) == [(0, 12)]
+    assert chunk_bounds(12, 6) == [(0, 6), (6, 12)]
+    assert chunk_bounds(12, (2, 4, 6)) == [(0, 2), (2, 6), (6, 12)]
+    assert chunk_bounds(8, (2, 4, 6)) == [(0, 2), (2, 6), (6, 8)]
+    assert chunk_bounds(5, (2,)) == [(0, 2), (2, 4), (4, 5)]
