@@ -207,7 +207,12 @@ typedef struct {
 int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* args, void* stream);
 
 /* bwd: dx(f32) = LN'(dy) + dres; dx_bf optional bf16 copy; partials
- * [maeclip_ln_bwd_partial_rows(M)][D] of dgamma, dbeta, colsum(dx). */
+ * [maeclip_ln_bwd_partial_rows(M)][D] of dgamma, dbeta, colsum(dx).
+ * dres_pool (instead of dres, optional): the residual gradient is the
+ * backward of timm's global_pool="avg" over pool_n tokens per sample, read
+ * from dres_pool [M / pool_n][D]: row r gets dres_pool[r / pool_n] / (pool_n - 1)
+ * for r % pool_n != 0 and 0 for the prefix (cls) token -- the pool backward
+ * fused into the LN backward, no [M, D] residual tensor in HBM. */
 typedef struct {
   const void* dy;
   int32_t dy_dtype;
@@ -224,6 +229,8 @@ typedef struct {
   float* dbeta_partial;
   float* dx_colsum_partial;
   int64_t M, D, ldx, lddy, lddx;
+  const float* dres_pool;
+  int64_t pool_n;
 } maeclip_ln_bwd_args;
 int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* args, void* stream);
 int32_t maeclip_ln_bwd_partial_rows(int64_t M);

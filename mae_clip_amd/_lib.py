@@ -51,7 +51,8 @@ class LnBwdArgs(C.Structure):
                 ("mean", c_vp), ("rstd", c_vp), ("gamma", c_vp), ("dres", c_vp),
                 ("dx", c_vp), ("dx_bf", c_vp), ("lddx_bf", c_i64),
                 ("dgamma_partial", c_vp), ("dbeta_partial", c_vp), ("dx_colsum_partial", c_vp),
-                ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("lddy", c_i64), ("lddx", c_i64)]
+                ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("lddy", c_i64), ("lddx", c_i64),
+                ("dres_pool", c_vp), ("pool_n", c_i64)]
 
 
 class MtEntry(C.Structure):

@@ -227,10 +227,9 @@ __device__ __forceinline__ v8s tr_frag(const char* img, int rb, int c0, int lane
   return r;
 }
 __device__ __forceinline__ v8s pack_p(const v4f& a, const v4f& b) {
-  v8s r;
-  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
-  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
-  return r;
+  // four v_cvt_pk_bf16_f32 (RNE), one per pair
+  const v4u u = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(v8s, u);
 }
 
 // D[c][col] += sum over 32 rows (rb..rb+31) of X[row][c] * P[row][col], where
@@ -310,46 +309,64 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
     for (int dt = 0; dt < HD / 16; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
 
     for (int kc = 0; kc < npad; kc += 64) {
+      // 32-key halves of this chunk that hold real keys (wave-uniform): the
+      // last chunk of n = 197 computes keys 192..223 only, not 192..255
+      const int nh = min(2, (n - kc + 31) >> 5);
       v4f s[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s[t] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (t < 2 * nh) {
 #pragma unroll
-        for (int ks = 0; ks < HD / 32; ++ks) {
-          RowFrag<T, HD> kf;
-          kf.lds(Kimg, kc + 16 * t, ks, lane);
-          s[t] = mma32(kf, qf[ks], s[t]);
+          for (int ks = 0; ks < HD / 32; ++ks) {
+            RowFrag<T, HD> kf;
+            kf.lds(Kimg, kc + 16 * t, ks, lane);
+            s[t] = mma32(kf, qf[ks], s[t]);
+          }
         }
       }
+      // p = 2^(s*c - m): the scale c > 0 is folded into the exponent's fma,
+      // the running max is taken on the raw scores (chunks with padding or
+      // masked keys add the -1e30 key bias first)
+      const bool masked = kc + 64 > n || a.key_mask;   // wave-uniform
       float mloc = NEG_BIG;
-      if (kc + 64 > n || a.key_mask) {  // wave-uniform: padding / key-mask chunk
+      if (masked) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
+          if (t < 2 * nh) {
+            const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) s[t][i] = fmaf(s[t][i], c, km[i]);
+            for (int i = 0; i < 4; ++i) s[t][i] = fmaf(s[t][i], c, km[i]);
+          }
         }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (t < 2 * nh)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
       } else {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) s[t] *= c;
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
+        mloc *= c;
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
       mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float mnew = fmaxf(m, mloc);
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float lp = 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        if (t < 2 * nh) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __builtin_amdgcn_exp2f(s[t][i] - mnew);
-          lp += p;
-          s[t][i] = p;
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(masked ? s[t][i] - mnew : fmaf(s[t][i], c, -mnew));
+            lp += p;
+            s[t][i] = p;
+          }
         }
+      }
       lsum = lsum * alpha + lp;
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
@@ -357,17 +374,19 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
       if (drop) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
+          if (t < 2 * nh)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = kc + 16 * t + 4 * g + i;
-            s[t][i] = dropout_keep(mc_step_seed(a.seed, a.step_ptr), bh, q, key, thr) ? s[t][i] * dscale : 0.f;
-          }
+            for (int i = 0; i < 4; ++i) {
+              const int key = kc + 16 * t + 4 * g + i;
+              s[t][i] = dropout_keep(mc_step_seed(a.seed, a.step_ptr), bh, q, key, thr) ? s[t][i] * dscale : 0.f;
+            }
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
+        if (s2 < nh)
 #pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-          o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
+          for (int dt = 0; dt < HD / 16; ++dt)
+            o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
     }
     lsum += __shfl_xor(lsum, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);

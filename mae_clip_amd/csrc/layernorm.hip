@@ -126,6 +126,16 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
     load_row<NC, GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
     load_row<NC, XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
     if (a.dres) load_row<NC, float>(dr, a.dres + row * a.lddx, D, lane);
+    const bool pool = a.dres_pool != nullptr;
+    if (pool) {   // global_pool="avg" backward: 1/(n-1) of the pooled gradient, 0 for the cls row
+      load_row<NC, float>(dr, a.dres_pool + (row / a.pool_n) * D, D, lane);
+      const bool cls = row % a.pool_n == 0;
+      const float den = (float)(a.pool_n - 1);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dr[c][j] = cls ? 0.f : dr[c][j] / den;
+    }
     const float mean = a.mean[row], rstd = a.rstd[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -150,7 +160,7 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float d = rstd * (dy[c][j] * gm[c][j] - s1 - x[c][j] * s2);
-        if (a.dres) d += dr[c][j];
+        if (a.dres || pool) d += dr[c][j];
         o[j] = d;
         pc[c][j] += d;
       }
@@ -214,6 +224,8 @@ extern "C" int32_t maeclip_ln_bwd_partial_rows(int64_t M) { return ln_bwd_grid(M
 extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
   MC_CHECK_ARG(a && a->dy && a->x && a->mean && a->rstd && a->gamma && a->dx, "maeclip_ln_bwd: null pointer");
   MC_CHECK_ARG(a->D > 0 && a->D <= MAXC * 256 && a->D % 4 == 0, "maeclip_ln_bwd: D unsupported");
+  MC_CHECK_ARG(!a->dres_pool || (!a->dres && a->pool_n > 1 && a->M % a->pool_n == 0),
+               "maeclip_ln_bwd: dres_pool needs pool_n > 1 dividing M (and no dres)");
   if (a->M == 0) return 0;
   dim3 grid((unsigned)ln_bwd_grid(a->M));
   hipStream_t s = (hipStream_t)stream;

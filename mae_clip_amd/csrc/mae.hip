@@ -89,6 +89,35 @@ __global__ void __launch_bounds__(NTH) patch_gather_kernel(const maeclip_patch_a
   }
 }
 
+// The same rows with one lane per 4 pixels (p % 4 == 0): lane -> (segment,
+// quarter), segments (row j, c, ky) ordered with ky fastest, so the p/4 lanes
+// of a segment read one contiguous 4p-byte run of an image row together, and
+// at p = 16 one wave covers a whole (row, c) block: 16 image-row runs of 64 B
+// in, 256 consecutive output elements out (the one-lane-per-run kernel below
+// touches 64 rows with 16 B per lane per load instruction)
+template <typename OT>
+__global__ void __launch_bounds__(NTH) patch_gather4_kernel(const maeclip_patch_args a) {
+  const int64_t t = (int64_t)blockIdx.x * NTH + threadIdx.x;
+  const int p = a.p, C = a.C, S = a.S, w = S / p, L = w * w, Q = p >> 2;
+  const int64_t nt = (int64_t)a.B * a.keep * C * p * Q;
+  if (t >= nt) return;
+  const int qr = (int)(t % Q);
+  const int64_t seg = t / Q;
+  const int ky = (int)(seg % p);
+  const int c = (int)((seg / p) % C);
+  const int64_t row = seg / ((int64_t)p * C);
+  const int b = (int)(row / a.keep), j = (int)(row % a.keep);
+  const int l = a.ids_shuffle ? a.ids_shuffle[(int64_t)b * L + j] : j;
+  const int py = l / w, px = l % w;
+  const float* src = a.img + (((int64_t)b * C + c) * S + (py * p + ky)) * S + px * p + 4 * qr;
+  OT* dst = (OT*)a.out + row * a.ld_out + (int64_t)c * p * p + ky * p + 4 * qr;
+  st4<OT>(dst, *(const v4f*)src);
+  if (c == 0 && ky == 0) {   // zero pad columns [C*p*p, ld_out): the segment's lanes share them
+    OT* prow = (OT*)a.out + row * a.ld_out;
+    for (int64_t k = (int64_t)C * p * p + qr; k < a.ld_out; k += Q) st_from_f<OT>(prow + k, 0.f);
+  }
+}
+
 // patch rows of the visible patches from the decoded uint8 HWC pixels, with
 // A.Normalize + the HWC->CHW permute (dataset.py:49, :34) folded in: one
 // thread per (row, ky) reads the p*C contiguous bytes of that patch row
@@ -499,9 +528,20 @@ extern "C" int32_t maeclip_patch_gather(const maeclip_patch_args* a, void* strea
     return 0;
   }
   const int64_t nseg = (int64_t)a->B * a->keep * a->C * a->p;
+  hipStream_t st = (hipStream_t)stream;
+  const int ob = a->dtype == MAECLIP_BF16 ? 2 : 4;
+  if (a->p % 4 == 0 && a->S % 4 == 0 && ((uintptr_t)a->img & 15) == 0 && ((uintptr_t)a->out & 7) == 0 &&
+      (a->ld_out * ob) % 8 == 0) {
+    const int64_t nt = nseg * (a->p / 4);
+    dim3 grid((unsigned)((nt + NTH - 1) / NTH));
+    if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((patch_gather4_kernel<bf16_t>), grid, dim3(NTH), 0, st, *a);
+    else hipLaunchKernelGGL((patch_gather4_kernel<float>), grid, dim3(NTH), 0, st, *a);
+    MC_CHECK_LAUNCH("maeclip_patch_gather");
+    return 0;
+  }
   dim3 grid((unsigned)((nseg + NTH - 1) / NTH));
-  if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((patch_gather_kernel<bf16_t>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
-  else hipLaunchKernelGGL((patch_gather_kernel<float>), grid, dim3(NTH), 0, (hipStream_t)stream, *a);
+  if (a->dtype == MAECLIP_BF16) hipLaunchKernelGGL((patch_gather_kernel<bf16_t>), grid, dim3(NTH), 0, st, *a);
+  else hipLaunchKernelGGL((patch_gather_kernel<float>), grid, dim3(NTH), 0, st, *a);
   MC_CHECK_LAUNCH("maeclip_patch_gather");
   return 0;
 }

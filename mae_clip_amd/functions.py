@@ -338,17 +338,20 @@ class EncoderHeadFn(torch.autograd.Function):
         fcn_w, mn_w = ctx.w
         B, n, D = x.shape
         dpooled, _, pg, pb, _ = K.ln_bwd(gfeat.contiguous(), pooled, fm, fr, fcn_w)
-        dx = K.pool_bwd(dpooled, n)
         fcn_b, mn_b = ctx.b
         ar = ctx.arena
         g_fw, g_fb = _reduce(pg, out=gout(ar, fcn_w)), _reduce(pb, out=gout(ar, fcn_b))
         g_mw = g_mb = None
         if ctx.mae and glatent is not None:
+            # the avg-pool backward rides in the mae_norm LN backward as its
+            # residual gradient (no [B, n, D] pool-gradient tensor in HBM)
             lm, lr = ctx.lstats
             dx2, _, pg2, pb2, _ = K.ln_bwd(glatent.contiguous(), x.view(B * n, D), lm, lr, mn_w,
-                                           dres=dx.view(B * n, D))
+                                           dres_pool=dpooled, pool_n=n)
             dx = dx2.view(B, n, D)
             g_mw, g_mb = _reduce(pg2, out=gout(ar, mn_w)), _reduce(pb2, out=gout(ar, mn_b))
+        else:
+            dx = K.pool_bwd(dpooled, n)
         return dx, None, g_fw, g_fb, g_mw, g_mb
 
 

@@ -356,9 +356,12 @@ def ln_bwd_partial_rows(M: int) -> int:
     return int(L.lib().maeclip_ln_bwd_partial_rows(M))
 
 
-def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False):
-    """Returns (dx f32, dx_bf16, dgamma_partial, dbeta_partial, dx_colsum_partial)."""
-    _dev(dy, x, mean, rstd, gamma, dres)
+def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False,
+           dres_pool=None, pool_n=0):
+    """Returns (dx f32, dx_bf16, dgamma_partial, dbeta_partial, dx_colsum_partial).
+    dres_pool [M / pool_n, D]: residual gradient = the avg-pool backward of it
+    (1/(pool_n-1) on every non-cls row), fused instead of a dres tensor."""
+    _dev(dy, x, mean, rstd, gamma, dres, dres_pool)
     M, D = x.shape
     dev = x.device
     G = ln_bwd_partial_rows(M)
@@ -370,7 +373,8 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
     a = L.LnBwdArgs(dy=dy.data_ptr(), dy_dtype=_dt(dy), x=x.data_ptr(), x_dtype=_dt(x), mean=mean.data_ptr(),
                     rstd=rstd.data_ptr(), gamma=gamma.data_ptr(), dres=_ptr(dres), dx=dx.data_ptr(), dx_bf=_ptr(dxb),
                     lddx_bf=D, dgamma_partial=_ptr(pg), dbeta_partial=_ptr(pb), dx_colsum_partial=_ptr(pc),
-                    M=M, D=D, ldx=x.stride(0), lddy=dy.stride(0), lddx=D)
+                    M=M, D=D, ldx=x.stride(0), lddy=dy.stride(0), lddx=D, dres_pool=_ptr(dres_pool),
+                    pool_n=int(pool_n))
     _call("maeclip_ln_bwd", C.byref(a), _stream())
     return dx, dxb, pg, pb, pc
 

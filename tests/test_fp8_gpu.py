@@ -160,8 +160,8 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
     assert w8b < FP8_TOL[2], w8b
 
 
-FP8_TOL = (3e-2, 0.2, 0.15)
-BF16_C4_TOL = 0.1
+FP8_TOL = (1.5e-2, 0.2, 0.2)     # measured r03: 0.0076, 0.106, 0.106
+BF16_C4_TOL = 1.25e-2           # measured r03: 0.0061
 
 
 def test_batched_weight_quantisation_matches_single(dev):
