@@ -844,7 +844,11 @@ int gemm4_ncu() {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  return ncu;
+  // diagnostic: MAECLIP_GEMM_GRID caps the persistent grid of plain launches
+  // (contention scans, tools/gemm_grid_scan.py); unset in production
+  const char* e = getenv("MAECLIP_GEMM_GRID");
+  const int cap = (e && *e) ? atoi(e) : 0;
+  return cap > 0 && cap < ncu ? cap : ncu;
 }
 
 // 192-row tiles when they need fewer full-tile rounds of the persistent grid;
