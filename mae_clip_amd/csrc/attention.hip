@@ -325,10 +325,11 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
           }
         }
       }
-      // p = 2^(s*c - m): the scale c > 0 is folded into the exponent's fma,
-      // the running max is taken on the raw scores (chunks with padding or
-      // masked keys add the -1e30 key bias first)
-      const bool masked = kc + 64 > n || a.key_mask;   // wave-uniform
+      // p = 2^(s*c - m): on chunks without padding / masked keys the scale
+      // c > 0 rides in the exponent's fma and the running max is taken on the
+      // raw scores; other chunks add the -1e30 key bias to c*s first. The
+      // branches are wave-uniform and hoisted out of the element loops.
+      const bool masked = kc + 64 > n || a.key_mask;
       float mloc = NEG_BIG;
       if (masked) {
 #pragma unroll
@@ -336,14 +337,12 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
           if (t < 2 * nh) {
             const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) s[t][i] = fmaf(s[t][i], c, km[i]);
+            for (int i = 0; i < 4; ++i) {
+              s[t][i] = fmaf(s[t][i], c, km[i]);
+              mloc = fmaxf(mloc, s[t][i]);
+            }
           }
         }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (t < 2 * nh)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
       } else {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -355,13 +354,16 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float mnew = fmaxf(m, mloc);
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      // one fma per element either way: masked chunks hold c*s + bias already
+      // (cc = 1), the others raw scores (cc = c)
+      const float cc = masked ? 1.f : c, nm = -mnew;
       float lp = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < 2 * nh) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = __builtin_amdgcn_exp2f(masked ? s[t][i] - mnew : fmaf(s[t][i], c, -mnew));
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], cc, nm));
             lp += p;
             s[t][i] = p;
           }

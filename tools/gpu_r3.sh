@@ -42,8 +42,11 @@ for s in $STEPS; do
         python tools/gemm_bench.py > gpurun_out/hbprof_${TAG}.log 2>&1 || { tail -30 gpurun_out/hbprof_${TAG}.log; exit 1; }
       tail -3 gpurun_out/hbprof_${TAG}.log ;;
     gridscan)
-      timeout -k 10 200 python -u tools/gemm_grid_scan.py > gpurun_out/gridscan_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gridscan_${TAG}.jsonl; exit 1; }
+      MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_dev.so timeout -k 10 200 python -u tools/gemm_grid_scan.py > gpurun_out/gridscan_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gridscan_${TAG}.jsonl; exit 1; }
       cat gpurun_out/gridscan_${TAG}.jsonl ;;
+    abattn)
+      timeout -k 10 400 bash tools/ab_attn_libs.sh mae_clip_amd/libmaeclip_base.so mae_clip_amd/libmaeclip_dev.so > gpurun_out/abattn_${TAG}.txt 2>&1 || { tail -30 gpurun_out/abattn_${TAG}.txt; exit 1; }
+      cat gpurun_out/abattn_${TAG}.txt ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
         python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
