@@ -129,8 +129,11 @@ __device__ __forceinline__ void mma64(v4f (&acc)[8][8], const Frags& f) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 8; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the host pass cannot type-check AGPR constraints
       asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
+#endif
+    }
 }
 
 // Epilogue of a wave's 128 x 128 block. Fragment (i, j): rows m0 + 128 wm +
@@ -181,7 +184,9 @@ __device__ __forceinline__ void epilogue5(const maeclip_gemm_args& args, v4f (&a
   // uniform scalars re-read from the kernel arguments here (s_load): kept live
   // across the K-loop they would sit in spilled VGPRs
   float alpha = args.alpha, beta = args.beta;
+#if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("" : "+s"(alpha), "+s"(beta));
+#endif
   // column sums only for the MLP dgrad (mul-aux) epilogue, their one user:
   // 32 more live VGPRs would push the other epilogues into spills
   constexpr bool CSUM = EPI == EPI_MUL_AUX;
@@ -311,7 +316,7 @@ __device__ __forceinline__ void epilogue5(const maeclip_gemm_args& args, v4f (&a
 }
 
 template <int LA, int LB, typename OutT, int EPI>
-__global__ void __launch_bounds__(NTH5, 1) gemm5_kernel(const maeclip_gemm_args args) {
+__device__ __forceinline__ void gemm5_body(const maeclip_gemm_args& args) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -356,7 +361,9 @@ __global__ void __launch_bounds__(NTH5, 1) gemm5_kernel(const maeclip_gemm_args 
     // few VALU ops) rather than kept live across the loop nest, where the
     // allocator spills it and the reload would wait behind the DMA in vmcnt.
     int ln = lane;
+#if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(ln));
+#endif
     const int vA = voff5<LA>(args.lda, 0, wave, ln);
     const int vB = voff5<LB>(args.ldb, 0, wave, ln);
 #pragma unroll
@@ -436,6 +443,13 @@ __global__ void __launch_bounds__(NTH5, 1) gemm5_kernel(const maeclip_gemm_args 
     read_frags<LA, LB>(f0, smem + (g & 1) * STAGE, 0, wm, wn, lane);
     after_epi = true;
   }
+}
+
+// thin kernel over a device body (the host pass then instantiates the kernel
+// stub; with the body inline in the __global__ template it did not)
+template <int LA, int LB, typename OutT, int EPI>
+__global__ void __launch_bounds__(NTH5, 1) gemm5_kernel(const maeclip_gemm_args args) {
+  gemm5_body<LA, LB, OutT, EPI>(args);
 }
 
 int ncu5() {
