@@ -32,8 +32,6 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
-int gemm_v5(const maeclip_gemm_args& a, hipStream_t s);
-bool gemm_v5_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_small_ok(const maeclip_gemm_args& a);
 int64_t gemm_small_workspace(const maeclip_gemm_args& a);
@@ -430,13 +428,7 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   int rc = 1;
   // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
   // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
-  // v5 (4 waves, 128x128 accumulators per wave in AGPRs): opt-in while it is
-  // being measured against v4 (MAECLIP_GEMM_V5=1)
-  const char* v5e = getenv("MAECLIP_GEMM_V5");   // per call: the tests switch it
-  const bool v5 = v5e && atoi(v5e) != 0;
-  if (forced == 0 && v5 && maeclip::gemm_v5_ok(*a))
-    rc = maeclip::gemm_v5(*a, s);
-  else if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
+  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
     rc = maeclip::gemm_v4(*a, s);
   else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
            (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))

@@ -38,15 +38,13 @@ def test_gemm_layouts(dev, dtype, lay, mnk):
     assert err / scale < (2e-6 if dtype == torch.float32 else 2e-5) * math.sqrt(Kd), (err, scale)
 
 
-@pytest.mark.parametrize("kern", ["bm192", "v5"])
 @pytest.mark.parametrize("b_lay", [0, 1])
 @pytest.mark.parametrize("mnk", [(12800, 768, 768), (1000, 520, 192), (50000, 512, 256), (192, 256, 64), (193, 264, 128),
                                  (12800, 3072, 768), (6400, 768, 3072), (300, 264, 64)])
-def test_gemm_bm192_v5(dev, b_lay, mnk, kern, monkeypatch):
-    """192-row tiles of the v4 kernel (forced) and the 4-wave v5 kernel
-    (opt-in): ragged M / N, one tile, several persistent tiles per block
+def test_gemm_bm192(dev, b_lay, mnk, monkeypatch):
+    """192-row tiles of the v4 kernel (forced): ragged M / N, one tile, several persistent tiles per block
     (M = 50000: 261 x 2 tiles on 256 CUs), one K-tile, KC x KC and KC x RC."""
-    monkeypatch.setenv("MAECLIP_GEMM_BM" if kern == "bm192" else "MAECLIP_GEMM_V5", "192" if kern == "bm192" else "1")
+    monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
     M, N, Kd = mnk
     A = _rand((M, Kd), torch.bfloat16, dev, seed=1)
     B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, seed=2)
@@ -61,14 +59,14 @@ def test_gemm_bm192_v5(dev, b_lay, mnk, kern, monkeypatch):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M", [300, 700])   # fp32: 32x32-tile small kernel / 128x128 MFMA kernel
-@pytest.mark.parametrize("bm", ["auto", "192", "v5"])
+@pytest.mark.parametrize("bm", ["auto", "192"])
 def test_gemm_epilogues(dev, dtype, M, bm, monkeypatch):
     """bm = "192": every epilogue on 192-row tiles (forced; colsum launches keep
-    256); "v5": the 4-wave kernel (opt-in; colsum only with mul-aux)."""
+    256)."""
     if bm != "auto":
         if dtype == torch.float32:
-            pytest.skip("192-row tiles / v5: bf16 operands")
-        monkeypatch.setenv("MAECLIP_GEMM_BM" if bm == "192" else "MAECLIP_GEMM_V5", "192" if bm == "192" else "1")
+            pytest.skip("192-row tiles: bf16 operands")
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
     N, Kd = 384, 256
     x = _rand((M, Kd), dtype, dev, seed=3)
     w = _rand((N, Kd), dtype, dev, scale=0.05, seed=4)

@@ -47,12 +47,6 @@ for s in $STEPS; do
     abattn)
       timeout -k 10 400 bash tools/ab_attn_libs.sh mae_clip_amd/libmaeclip_base.so mae_clip_amd/libmaeclip_dev.so > gpurun_out/abattn_${TAG}.txt 2>&1 || { tail -30 gpurun_out/abattn_${TAG}.txt; exit 1; }
       cat gpurun_out/abattn_${TAG}.txt ;;
-    v5ab)    # GEMM v4 vs v5 on the production shapes (default + epilogue sets), one library
-      for v in 0 1; do for set in "" epi; do
-        MAECLIP_GEMM_V5=$v GEMM_SET=$set timeout -k 10 200 python -u tools/gemm_bench.py > gpurun_out/v5ab_${TAG}_${v}${set}.jsonl 2>&1 \
-          || { tail -30 gpurun_out/v5ab_${TAG}_${v}${set}.jsonl; exit 1; }
-      done; done
-      python tools/v5ab_table.py gpurun_out/v5ab_${TAG}_0.jsonl gpurun_out/v5ab_${TAG}_1.jsonl gpurun_out/v5ab_${TAG}_0epi.jsonl gpurun_out/v5ab_${TAG}_1epi.jsonl ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
         python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
