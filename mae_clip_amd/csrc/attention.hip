@@ -260,7 +260,103 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t bh, int q, 
 }
 
 // ============================================================== forward
-template <typename T, int HD>
+// max over the four 16-lane rows (the lanes l, l^16, l^32, l^48 of a query):
+// two permlane swaps (VALU) instead of two ds_bpermute round trips
+__device__ __forceinline__ float max4rows(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum4rows(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+struct FwdDrop {
+  uint64_t seed, bh;
+  uint32_t thr;
+  float scale;
+};
+
+// One 64-key chunk of a 16-query tile with its shape fixed at compile time, so
+// the body is straight-line code the scheduler can interleave (the runtime
+// per-32-key / mask / dropout branches of a generic body split it into ~30
+// basic blocks with an MFMA or a few VALU ops each). NH: 32-key halves that
+// hold real keys (1 only for the tail chunk of n = 197: keys 192..223);
+// MASKED: add the key bias (padding keys, DistilBERT's key mask) -- the scale
+// c > 0 then rides in the bias fma, otherwise in the exponent's fma and the
+// running max is taken on the raw scores.
+template <typename T, int HD, int NH, bool MASKED, bool DROP>
+__device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, const float* kmask, int kc,
+                                          const RowFrag<T, HD> (&qf)[HD / 32], float c, float& m, float& lsum,
+                                          v4f (&o)[HD / 16], int lane, const FwdDrop& dr, int q) {
+  const int g = lane >> 4;
+  v4f s[2 * NH];
+#pragma unroll
+  for (int t = 0; t < 2 * NH; ++t) {
+    s[t] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HD / 32; ++ks) {
+      RowFrag<T, HD> kf;
+      kf.lds(Kimg, kc + 16 * t, ks, lane);
+      s[t] = mma32(kf, qf[ks], s[t]);
+    }
+  }
+  float mloc = NEG_BIG;
+  if (MASKED) {
+#pragma unroll
+    for (int t = 0; t < 2 * NH; ++t) {
+      const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[t][i] = fmaf(s[t][i], c, km[i]);
+        mloc = fmaxf(mloc, s[t][i]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2 * NH; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
+    mloc *= c;
+  }
+  mloc = max4rows(mloc);
+  const float mnew = fmaxf(m, mloc);
+  const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+  const float cc = MASKED ? 1.f : c, nm = -mnew;
+  float lp = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2 * NH; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], cc, nm));
+      lp += p;
+      s[t][i] = p;
+    }
+  lsum = fmaf(lsum, alpha, lp);
+#pragma unroll
+  for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
+  m = mnew;
+  if (DROP) {
+#pragma unroll
+    for (int t = 0; t < 2 * NH; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kc + 16 * t + 4 * g + i;
+        s[t][i] = dropout_keep(dr.seed, dr.bh, q, key, dr.thr) ? s[t][i] * dr.scale : 0.f;
+      }
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < NH; ++s2)
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt)
+      o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
+}
+
+template <typename T, int HD, bool DROP>
 __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
@@ -290,10 +386,15 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
   ASTAMP(1);
 
   const float c = a.scale * LOG2E;
-  const bool drop = a.dropout_p > 0.f;
-  const uint32_t thr = (uint32_t)((double)a.dropout_p * 4294967296.0);
-  const float dscale = drop ? 1.f / (1.f - a.dropout_p) : 1.f;
-  const uint64_t bh = (uint64_t)b * H + h;
+  FwdDrop dr{};
+  if (DROP) {
+    dr.seed = mc_step_seed(a.seed, a.step_ptr);
+    dr.bh = (uint64_t)b * H + h;
+    dr.thr = (uint32_t)((double)a.dropout_p * 4294967296.0);
+    dr.scale = 1.f / (1.f - a.dropout_p);
+  }
+  // chunks whose 64 keys are all real and unmasked run the bias-free body
+  const int nfull = a.key_mask ? 0 : n >> 6;
 
   const int nqt = (n + 15) >> 4;
   for (int qt = wave; qt < nqt; qt += NW) {
@@ -308,90 +409,14 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
 
-    for (int kc = 0; kc < npad; kc += 64) {
-      // 32-key halves of this chunk that hold real keys (wave-uniform): the
-      // last chunk of n = 197 computes keys 192..223 only, not 192..255
-      const int nh = min(2, (n - kc + 31) >> 5);
-      v4f s[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s[t] = v4f{0.f, 0.f, 0.f, 0.f};
-        if (t < 2 * nh) {
-#pragma unroll
-          for (int ks = 0; ks < HD / 32; ++ks) {
-            RowFrag<T, HD> kf;
-            kf.lds(Kimg, kc + 16 * t, ks, lane);
-            s[t] = mma32(kf, qf[ks], s[t]);
-          }
-        }
-      }
-      // p = 2^(s*c - m): on chunks without padding / masked keys the scale
-      // c > 0 rides in the exponent's fma and the running max is taken on the
-      // raw scores; other chunks add the -1e30 key bias to c*s first. The
-      // branches are wave-uniform and hoisted out of the element loops.
-      const bool masked = kc + 64 > n || a.key_mask;
-      float mloc = NEG_BIG;
-      if (masked) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (t < 2 * nh) {
-            const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              s[t][i] = fmaf(s[t][i], c, km[i]);
-              mloc = fmaxf(mloc, s[t][i]);
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
-        mloc *= c;
-      }
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float mnew = fmaxf(m, mloc);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-      // one fma per element either way: masked chunks hold c*s + bias already
-      // (cc = 1), the others raw scores (cc = c)
-      const float cc = masked ? 1.f : c, nm = -mnew;
-      float lp = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < 2 * nh) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], cc, nm));
-            lp += p;
-            s[t][i] = p;
-          }
-        }
-      }
-      lsum = lsum * alpha + lp;
-#pragma unroll
-      for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
-      m = mnew;
-      if (drop) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (t < 2 * nh)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int key = kc + 16 * t + 4 * g + i;
-              s[t][i] = dropout_keep(mc_step_seed(a.seed, a.step_ptr), bh, q, key, thr) ? s[t][i] * dscale : 0.f;
-            }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-        if (s2 < nh)
-#pragma unroll
-          for (int dt = 0; dt < HD / 16; ++dt)
-            o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
+    int kc = 0;
+    for (; kc < 64 * nfull; kc += 64) fwd_chunk<T, HD, 2, false, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
+    for (; kc < npad; kc += 64) {
+      // 32-key halves of this chunk that hold real keys (wave-uniform)
+      if (n - kc > 32) fwd_chunk<T, HD, 2, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
+      else fwd_chunk<T, HD, 1, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
     }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
+    lsum = sum4rows(lsum);
     const float inv = 1.f / lsum;
     if (qok) {
       T* orow = (T*)a.o + ((int64_t)b * n + q) * a.ld_o + h * HD;
@@ -1040,9 +1065,12 @@ int bwd_two(int n, int nw, size_t lds4, size_t lds2) {
 
 template <typename T, int HD>
 int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
-  // one wave per 16-row tile (no idle waves), at most MAXW
+  // one wave per 16-row tile (no idle waves), at most MAXW; the forward
+  // spreads its tiles evenly over the rounds it needs (n = 197: 13 tiles on 7
+  // waves, not 8 waves of which 3 idle for the second round)
   const int tiles = (a.n + 15) / 16;
-  const int nw = tiles < MAXW ? tiles : MAXW;
+  const int rounds = (tiles + MAXW - 1) / MAXW;
+  const int nw = bwd ? (tiles < MAXW ? tiles : MAXW) : (tiles + rounds - 1) / rounds;
   const int nthreads = 64 * nw;
   size_t lds = bwd ? bwd_lds<T, HD>(a.n, nw) : fwd_lds<T, HD>(a.n);
   bool two = false;
@@ -1086,8 +1114,9 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     }
     if (!sds && !two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
-    if (lds > 65536) (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<T, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((attn_fwd_kernel<T, HD>), grid, dim3(nthreads), lds, s, a);
+    auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true> : attn_fwd_kernel<T, HD, false>;
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, grid, dim3(nthreads), lds, s, a);
   }
   MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");
   return 0;
