@@ -787,14 +787,6 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     kf[kt] = *(const v8s*)kr;
     vf[kt] = *(const v8s*)(kr + HH);
   }
-  bf16_t kraw[2][8];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int key = min(kbase + 16 * (j >> 2) + 4 * g + (j & 3), n - 1);
-      kraw[dt][j] = qkv[(int64_t)key * a.ld_qkv + HH + h * HD + 16 * dt + l15];
-    }
   // Q, dO, O chunks: thread -> chunk slots tid and tid + NTH (4 per row)
   v4u vq[2], vd[2], vo[2];
   float ls[2];
@@ -838,6 +830,17 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     vs[j] += dpp_mov<0x114>(vs[j]);
     vs[j] += dpp_mov<0x118>(vs[j]);
   }
+  // K^T (the A operand of dQ^T) through this wave's dS tile, which is free
+  // until the first round: the wave's 32 K rows as a [32][HD] image (padding
+  // keys zero), read back transposed -- instead of 16 two-byte global loads
+  // per lane
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const bool kok = kbase + 16 * kt + l15 < n;
+    *(v8s*)(myds + I::chunk(16 * kt + l15, g)) = kok ? kf[kt] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) kT[dt] = tr_frag<HD>(myds, 0, 16 * dt, lane);
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const bool kok = kbase + 16 * kt + l15 < n;
@@ -847,11 +850,6 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     kf[kt] = t;
     vf[kt] = kok ? vf[kt] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
   }
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      kT[dt][j] = kbase + 16 * (j >> 2) + 4 * g + (j & 3) < n ? (short)kraw[dt][j] : (short)0;
   ASTAMP(7);
   __syncthreads();
   if (a.colsum_partial && (lane & 15) >= 12)
