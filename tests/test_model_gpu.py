@@ -120,8 +120,9 @@ def test_vitb_parity_fp32_vs_oracle(dev, cfg):
 
 
 # (loss rel, worst gradient rel-L2) bounds for the bf16 path vs the fp64 oracle:
-# about 2x the values measured on MI355X (profiles/r03/parity.json)
-BF16_TOL = {"C1": (2e-2, 1e-1), "C2": (2e-2, 1e-1)}
+# about 2x the values measured on MI355X (profiles/r03/parity.jsonl: C1 loss
+# 0.0052, grads 0.0138; C2 loss 0.0027, grads 0.0428)
+BF16_TOL = {"C1": (1.0e-2, 3.0e-2), "C2": (6.0e-3, 9.0e-2)}
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
@@ -129,7 +130,8 @@ def test_vitb_bf16_vs_oracle(dev, cfg):
     """The bench's bf16 production path at ViT-B shapes vs the fp64 oracle on
     identical weights (B = 4). Tolerances (bf16 GEMM operands, fp32
     accumulation and statistics; SURVEY.md §7 'Parity vs bf16'): loss within
-    2e-2 relative; every gradient within 1e-1 relative L2 of the oracle's."""
+    BF16_TOL[cfg][0] relative; every gradient within BF16_TOL[cfg][1]
+    relative L2 of the oracle's (about 2x the measured deviations)."""
     kw = VITB_C1 if cfg == "C1" else VITB_C2
     prod, ref = build_pair("bf16", **kw)
     prod.eval()
@@ -145,7 +147,7 @@ def test_vitb_bf16_vs_oracle(dev, cfg):
         rg = rp[name].grad
         e = ((p.grad.double().cpu() - rg).norm() / (rg.norm() + 1e-30)).item()
         worst = max(worst, e)
-        if not e < 1e-1:
+        if not e < BF16_TOL[cfg][1]:
             bad.append((e, name))
     record_parity(f"vitb_{cfg}_bf16_vs_oracle", loss_rel=rel, worst_grad_relL2=worst)
     assert rel < BF16_TOL[cfg][0], (loss.item(), rloss.item())
@@ -493,7 +495,7 @@ def test_vitl14_336_full_depth_bf16_vs_oracle(dev):
         rloss = ref(dict(batch, image=batch["image"].double())).item()
     rel = abs(loss.item() - rloss) / max(1.0, abs(rloss))
     record_parity("vitl14_336_full_depth_bf16_vs_oracle", loss_rel=rel, product=loss.item(), oracle=rloss)
-    assert rel < 2e-2, (loss.item(), rloss)
+    assert rel < 1e-3, (loss.item(), rloss)   # measured r03: 7.6e-6
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 template <int LAYOUT, bool LOAD>
@@ -44,7 +45,7 @@ __global__ void __launch_bounds__(512) k(unsigned short* C, int M, int N, int ti
   if (LOAD && acc[0] == 12345u) sink[0] = acc;
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int M = 50432, N = 2048, ld = N;
   unsigned short* C;
   v4u* sink;
@@ -52,7 +53,7 @@ int main() {
   hipMalloc(&sink, 64);
   hipMemset(C, 0, (size_t)M * ld * 2);
   const int tiles = (M / 256) * (N / 256);
-  const int G = 256, tpb = (tiles + G - 1) / G;
+  const int G = argc > 1 ? atoi(argv[1]) : 256, tpb = (tiles + 255) / 256;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
