@@ -69,9 +69,23 @@ def _trunc_normal_(t, std=0.02):
     nn.init.trunc_normal_(t, std=std, a=-2 * std, b=2 * std)
 
 
+# parameter -> its bf16 shadow (a view into a WeightCache buffer), kept as an
+# attribute of the parameter. The fused AdamW (optim.py) writes the shadow in
+# the same pass as the update, so a shadow stays equal to bf16(p) without a
+# cast launch; any other in-place change of p (load_state_dict, torch ops,
+# another optimizer) bumps p._version and the next refresh() casts again.
+def shadow_of(p):
+    return getattr(p, "_mc_bf16_shadow", None)
+
+
+def _set_shadow(p, view):
+    p._mc_bf16_shadow = view
+
+
 class WeightCache:
-    """bf16 shadows of the GEMM weights, refreshed by ONE multi-tensor cast
-    launch per forward (fp32 master weights stay the nn.Parameters).
+    """bf16 shadows of the GEMM weights: one multi-tensor cast launch when a
+    master weight changed outside the fused AdamW (which keeps the shadows
+    current itself, shadow_of); fp32 master weights stay the nn.Parameters.
 
     fp8=True (precision "fp8", C4): the transformer stacks' GEMM weights are
     also quantised once per forward from their fp32 masters (get_fp8): W with
@@ -82,6 +96,7 @@ class WeightCache:
         self.entries = []    # (param, shape2d)
         self.views = {}
         self.key = None
+        self.vers = None
         self.plan = None
         self.buf = None
         self.fp8 = fp8
@@ -109,6 +124,12 @@ class WeightCache:
         if dtype == torch.float32 or not self.entries:
             return
         key = tuple(p.data_ptr() for p, _ in self.entries)
+        vers = tuple(p._version for p, _ in self.entries)
+        if key == self.key and vers == self.vers and all(shadow_of(p) is self.views[id(p)] for p, _ in self.entries):
+            return   # every shadow is bf16(p): cast at the last refresh or written by the fused AdamW
+        for p, _ in self.entries:   # (another cache's shadows may have been the ones AdamW kept current)
+            if id(p) in self.views:
+                _set_shadow(p, self.views[id(p)])
         if key != self.key:
             dev = self.entries[0][0].device
             total = sum(p.numel() for p, _ in self.entries)
@@ -122,7 +143,10 @@ class WeightCache:
                 off += p.numel()
             self.plan = K.MultiTensorPlan(ents, dev)
             self.key = key
+            for p, _ in self.entries:
+                _set_shadow(p, self.views[id(p)])
         K.cast_multi(self.plan)
+        self.vers = vers
 
     def get(self, p: torch.Tensor, dtype, shape2d=None):
         if dtype == torch.float32:

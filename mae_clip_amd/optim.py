@@ -16,6 +16,7 @@ import torch
 
 from . import kernels as K
 from . import _lib as L
+from .modules import shadow_of
 
 
 class AdamW(torch.optim.Optimizer):
@@ -71,8 +72,11 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] = int(st["step"]) + 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                # the bf16 GEMM shadow of p (if any) is written in the same pass
+                sh = shadow_of(p)
+                sh = sh.data_ptr() if sh is not None and sh.numel() == p.numel() else None
                 entries.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                                None, p.numel(), st["step"]))
+                                sh, p.numel(), st["step"]))
                 device = p.device
             if not entries:
                 continue
