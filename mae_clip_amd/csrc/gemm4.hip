@@ -58,7 +58,8 @@ template <int BM> struct TileM {
   static constexpr int MI = BM / 64;                 // A fragments per wave per half
   static constexpr int HALF_A = BM / 2 * 128;        // bytes per A half image
   static constexpr int BUF_T = 2 * HALF_A + 2 * HALF;
-  static constexpr int LDS_T = 2 * BUF_T;
+  static constexpr int LDS_T = 2 * BUF_T;                      // operand stages
+  static constexpr int LDS_ALL = LDS_T + 8 * 4096;               // + epilogue scratch (8 waves x 4 KiB)
   __device__ static __forceinline__ int hoff(int h) { return h < 2 ? h * HALF_A : 2 * HALF_A + (h - 2) * HALF; }
 };
 
@@ -239,13 +240,46 @@ __device__ __forceinline__ void epilogue4_tile(float* __restrict__ t, v4f (&acc)
   }
 }
 
+// Epilogue in full-line row layout. The MFMA fragments (16 rows x 16 columns,
+// 4 consecutive columns per lane) would be stored / loaded as 16 rows x 64 B
+// per wave-instruction; tools/micro/store_layout.hip measured 2.3x the
+// per-CU rate for whole 128-B lines (8 rows x 128 B per instruction: 12.4 vs
+// 28.8 us for the same bytes on 64 CUs, loads alike), and the epilogue of
+// this kernel is bound by its CU's memory-instruction rate
+// (tools/gemm_grid_scan.py). So each 16-row chunk of the wave's 64-column
+// block goes through a 4 KiB per-wave LDS scratch (beside the operand stages:
+// the next tile's DMA is in flight in those) and comes back row-major:
+//   bf16 output (L8): lane -> row lane / 8 (+ 8 q), columns 8 (lane % 8) .. +7
+//                     = 16 B per lane, 8 rows x 128 B per instruction
+//   f32 output  (L4): lane -> row lane / 16 (+ 4 q), columns 4 (lane % 16) .. +3
+//                     = 16 B per lane, 4 rows x 256 B per instruction
+// and every epilogue operand (bias, aux, residual, C for beta, aux_out) is
+// read / written in that layout. Scratch: 16 rows x 256 B, 16-B unit u of
+// row r at unit u ^ r (conflict-free for the fragment writes and both read
+// layouts). The wave reads back only what it wrote (LDS is in order per wave).
+//
+// vmcnt is in-order on CDNA: a load issued after a store can only be waited
+// for together with that store. So every load (aux, resid) of a chunk is
+// issued BEFORE the stores of the previous chunk, and the stores themselves
+// are never waited for here (they drain behind the next tile's main loop, see
+// the counted wait at the tile start: 2 bf16 / 4 f32 store instructions per
+// chunk, as many more for the GELU epilogues' aux_out).
+//
 // sa / sb (fp8 only): per-row dequantisation scale of A [M] and per-column
 // scale of B [N]; the product scales the accumulator before alpha / bias.
+constexpr int EPI_SCR = 4096;   // bytes of epilogue scratch per wave
+__device__ __forceinline__ int scr_off(int r, int u) { return r * 256 + ((u ^ r) << 4); }
+
 template <typename OutT, int EPI, bool F8 = false, int BM = 256>
 __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&acc)[BM / 32][4], int64_t z, int m0,
-                                          int n0, int wm, int wn, int lane, const float* __restrict__ sa = nullptr,
+                                          int n0, int wm, int wn, int lane, char* __restrict__ scr,
+                                          const float* __restrict__ sa = nullptr,
                                           const float* __restrict__ sb = nullptr) {
-  constexpr int NCH = BM / 32;   // row fragments (chunks) per wave: 8 (BM 256) or 6 (BM 192)
+  constexpr int NCH = BM / 32;               // 16-row chunks per wave: 8 (BM 256) or 6 (BM 192)
+  constexpr bool L8 = sizeof(OutT) == 2;
+  constexpr int RPI = L8 ? 8 : 4;            // rows per instruction
+  constexpr int NQ = 16 / RPI;               // instructions per chunk
+  constexpr int VPL = L8 ? 8 : 4;            // values per lane per instruction
   constexpr bool LOAD_AUX = EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   constexpr bool LOAD_RES = EPI == EPI_RESID || EPI == EPI_DGELU || EPI == EPI_MUL_AUX;
   const int M = (int)args.M, N = (int)args.N;
@@ -255,159 +289,153 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
   OutT* __restrict__ C = (OutT*)args.C + off;
   const float alpha = args.alpha, beta = args.beta;
   const bool has_res = LOAD_RES && args.resid != nullptr;
-  const int rbase = m0 + (BM / 2) * wm + (lane & 15);   // + 16 i (row fragment i = chunk)
-  const int cb0 = n0 + 64 * wn + 16 * (g & 1) + 8 * (g >> 1);   // + 32 ni
-  v4f bias8[2][2];
+  const int lr = L8 ? lane >> 3 : lane >> 4;                    // row of the lane within an instruction
+  const int n = n0 + 64 * wn + (L8 ? 8 * (lane & 7) : 4 * (lane & 15));
+  const bool nok = n < N;                                        // N % 8 == 0 on this path
+  const int nc = nok ? n : N - VPL;
+  const int rbase = m0 + (BM / 2) * wm + lr;                     // + 16 c + RPI q
+  float bias[VPL], csc[VPL];
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int n = min(cb0 + 32 * ni, N - 8);   // N % 8 == 0 on this path
-    bias8[ni][0] = args.bias ? *(const v4f*)(args.bias + n) : v4f{0.f, 0.f, 0.f, 0.f};
-    bias8[ni][1] = args.bias ? *(const v4f*)(args.bias + n + 4) : v4f{0.f, 0.f, 0.f, 0.f};
+  for (int v = 0; v < VPL; v += 4) {
+    const v4f bv = args.bias ? *(const v4f*)(args.bias + nc + v) : v4f{0.f, 0.f, 0.f, 0.f};
+    const v4f sv = F8 ? *(const v4f*)(sb + nc + v) : v4f{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bias[v + r] = bv[r];
+      csc[v + r] = sv[r] * alpha;
+    }
   }
-  // chunk c = row fragment i = c (hh = c >> 2); q = ni. The aux / residual
-  // reads of chunk c + PF - 1 are issued before chunk c is finished: PF - 1
-  // HBM round trips in flight instead of one (the main-loop operand registers
-  // are dead here, so the ring fits the 256-register budget).
+  // aux / residual of chunk c + PF - 1 issued before chunk c is finished
   constexpr int PF = GEMM4_EPI_PF;
-  v4u ax[PF][2];
-  v4f rs[PF][2][2];
+  typedef unsigned int auxv_t __attribute__((ext_vector_type(L8 ? 4 : 2)));
+  auxv_t ax[PF][NQ];
+  v4f rs[PF][NQ][VPL / 4];
   auto load_chunk = [&](int c, int buf) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = c, ni = q;
-      const int m = min(rbase + 16 * i, M - 1);
-      const int n = min(cb0 + 32 * ni, N - 8);
-      if (LOAD_AUX) ax[buf][q] = *(const v4u*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + n);
+    for (int q = 0; q < NQ; ++q) {
+      const int m = min(rbase + 16 * c + RPI * q, M - 1);
+      if (LOAD_AUX) ax[buf][q] = *(const auxv_t*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + nc);
       if (LOAD_RES && has_res) {
-        const float* rp = args.resid + off + (int64_t)m * args.ldr + n;
-        rs[buf][q][0] = *(const v4f*)rp;
-        rs[buf][q][1] = *(const v4f*)(rp + 4);
+        const float* rp = args.resid + off + (int64_t)m * args.ldr + nc;
+#pragma unroll
+        for (int v = 0; v < VPL / 4; ++v) rs[buf][q][v] = *(const v4f*)(rp + 4 * v);
       }
     }
   };
-  float csum[2][8];
+  float csum[VPL];
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) csum[ni][r] = 0.f;
+  for (int v = 0; v < VPL; ++v) csum[v] = 0.f;
   if (LOAD_AUX || LOAD_RES) {
 #pragma unroll
     for (int c = 0; c < PF - 1; ++c) load_chunk(c, c);
   }
+  // fragment -> scratch offsets of this lane (row lane & 15; units 8 ni + 4 (g & 1) + 2 (g >> 1) + e)
+  int wo[4];
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) wo[2 * ni + e] = scr_off(lane & 15, 8 * ni + 4 * (g & 1) + 2 * (g >> 1) + e);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if ((LOAD_AUX || LOAD_RES) && c + PF - 1 < NCH) load_chunk(c + PF - 1, (c + PF - 1) % PF);
     __builtin_amdgcn_sched_barrier(0);   // keep chunk c+1's loads ahead of chunk c's stores
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int i = c, ni = q;
-      const int m = rbase + 16 * i;
-      const int n = cb0 + 32 * ni;
-      v4f lo, hi;
-      if constexpr (F8) {
-        // dequantise: per-row A scale x per-column B scale (re-read per chunk
-        // from L1/L2: keeps the register budget of the aux epilogues)
-        const float sam = sa[min(m, M - 1)] * alpha;
-        const int nc = min(n, N - 8);
-        lo = acc[i][2 * ni] * (*(const v4f*)(sb + nc) * sam) + bias8[ni][0];
-        hi = acc[i][2 * ni + 1] * (*(const v4f*)(sb + nc + 4) * sam) + bias8[ni][1];
-      } else {
-        lo = acc[i][2 * ni] * alpha + bias8[ni][0];
-        hi = acc[i][2 * ni + 1] * alpha + bias8[ni][1];
-      }
-      if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
-        v4f dlo = lo, dhi = hi;   // GELU: aux_out <- pre-activation
-        if (EPI == EPI_GELU_D) {
-          dlo = gelu4_inplace(lo);
-          dhi = gelu4_inplace(hi);
-        } else {
+    for (int j = 0; j < 4; ++j) *(v4f*)(scr + wo[j]) = acc[c][j];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            lo[r] = gelu_f(lo[r]);
-            hi[r] = gelu_f(hi[r]);
-          }
+    for (int q = 0; q < NQ; ++q) {
+      const int R = lr + RPI * q;           // row within the chunk
+      const int m = rbase + 16 * c + RPI * q;
+      float x[VPL];
+#pragma unroll
+      for (int v = 0; v < VPL / 4; ++v) {
+        const v4f t = *(const v4f*)(scr + scr_off(R, L8 ? 2 * (lane & 7) + v : (lane & 15)));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[4 * v + r] = t[r];
+      }
+      const float rsc = F8 ? sa[min(m, M - 1)] : 1.f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) x[v] = F8 ? fmaf(x[v] * rsc, csc[v], bias[v]) : fmaf(x[v], alpha, bias[v]);
+      const bool ok = m < M && nok;
+      if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
+        float d[VPL];   // GELU: aux_out <- pre-activation; GELU_D: aux_out <- gelu'(pre)
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          float y, dy;
+          gelu_pair(x[v], y, dy);
+          d[v] = EPI == EPI_GELU_D ? dy : x[v];
+          x[v] = y;
         }
-        if (args.aux_out && m < M && n < N) {
-          v4u pk;
-          pk[0] = pack2bf(dlo[0], dlo[1]);
-          pk[1] = pack2bf(dlo[2], dlo[3]);
-          pk[2] = pack2bf(dhi[0], dhi[1]);
-          pk[3] = pack2bf(dhi[2], dhi[3]);
-          *(v4u*)((bf16_t*)args.aux_out + off + (int64_t)m * args.ldaux + n) = pk;
+        if (args.aux_out && ok) {
+          bf16_t* ap = (bf16_t*)args.aux_out + off + (int64_t)m * args.ldaux + n;
+          if (L8) {
+            const v4u pk = {pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4 % VPL], d[5 % VPL]),
+                            pack2bf(d[6 % VPL], d[7 % VPL])};
+            *(v4u*)ap = pk;
+          } else {
+            const v2u pk = {pack2bf(d[0], d[1]), pack2bf(d[2], d[3])};
+            *(v2u*)ap = pk;
+          }
         }
       }
       if (LOAD_AUX) {
-        const v4u pk = ax[c % PF][q];
-        if (EPI == EPI_MUL_AUX) {
+        const auxv_t pk = ax[c % PF][q];
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            lo[2 * r] *= __uint_as_float(pk[r] << 16);
-            lo[2 * r + 1] *= __uint_as_float(pk[r] & 0xffff0000u);
-            hi[2 * r] *= __uint_as_float(pk[2 + r] << 16);
-            hi[2 * r + 1] *= __uint_as_float(pk[2 + r] & 0xffff0000u);
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            lo[2 * r] *= gelu_grad_f(__uint_as_float(pk[r] << 16));
-            lo[2 * r + 1] *= gelu_grad_f(__uint_as_float(pk[r] & 0xffff0000u));
-            hi[2 * r] *= gelu_grad_f(__uint_as_float(pk[2 + r] << 16));
-            hi[2 * r + 1] *= gelu_grad_f(__uint_as_float(pk[2 + r] & 0xffff0000u));
+        for (int r = 0; r < VPL / 2; ++r) {
+          const float a0 = __uint_as_float(pk[r] << 16), a1 = __uint_as_float(pk[r] & 0xffff0000u);
+          if (EPI == EPI_MUL_AUX) {
+            x[2 * r] *= a0;
+            x[2 * r + 1] *= a1;
+          } else {
+            x[2 * r] *= gelu_grad_f(a0);
+            x[2 * r + 1] *= gelu_grad_f(a1);
           }
         }
       }
       if (LOAD_RES && has_res) {
-        lo += rs[c % PF][q][0];
-        hi += rs[c % PF][q][1];
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) x[v] += rs[c % PF][q][v / 4][v % 4];
       }
-      if (m < M && n < N) {
+      if (ok) {
         OutT* cp = C + (int64_t)m * args.ldc + n;
         if (beta != 0.f) {
-          lo += beta * ld4<OutT>(cp);
-          hi += beta * ld4<OutT>(cp + 4);
+#pragma unroll
+          for (int v = 0; v < VPL; v += 4) {
+            const v4f cv = ld4<OutT>(cp + v);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[v + r] += beta * cv[r];
+          }
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          csum[ni][r] += lo[r];
-          csum[ni][4 + r] += hi[r];
-        }
-        if (sizeof(OutT) == 2) {
-          v4u pk;
-          pk[0] = pack2bf(lo[0], lo[1]);
-          pk[1] = pack2bf(lo[2], lo[3]);
-          pk[2] = pack2bf(hi[0], hi[1]);
-          pk[3] = pack2bf(hi[2], hi[3]);
+        for (int v = 0; v < VPL; ++v) csum[v] += x[v];
+        if (L8) {
+          const v4u pk = {pack2bf(x[0], x[1]), pack2bf(x[2], x[3]), pack2bf(x[4 % VPL], x[5 % VPL]),
+                          pack2bf(x[6 % VPL], x[7 % VPL])};
           *(v4u*)cp = pk;
         } else {
-          *(v4f*)cp = lo;
-          *(v4f*)((float*)cp + 4) = hi;
+          *(v4f*)cp = v4f{x[0], x[1], x[2], x[3]};
         }
       }
     }
-    if (BM == 256 && (c & 3) == 3 && args.colsum_partial) {  // one partial row per 64-row group hh = c >> 2
-      const int hh = c >> 2;
+    if (BM == 256 && (c & 3) == 3 && args.colsum_partial) {   // one partial row per 64-row group
+      // the lanes holding the same columns: L8 lanes k + 8 j (row_ror 8 inside
+      // each 16-lane row, then the four rows), L4 lanes u + 16 j (the four rows)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int v = 0; v < VPL; ++v) {
+        float t = csum[v];
+        if (L8) t += dpp_mov<0x128>(t);
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+        t = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+        const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+        csum[v] = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+      }
+      const int mrow = m0 + 128 * wm + 64 * (c >> 2);
+      if (lane < (L8 ? 8 : 16) && mrow < M && nok) {
+        float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N + n;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          csum[ni][r] = row16_sum(csum[ni][r]);
-        }
-      const int mrow = m0 + 128 * wm + 64 * hh;
-      if ((lane & 15) == 0 && mrow < M) {
-        float* prow = args.colsum_partial + ((int64_t)z * ((M + 63) / 64) + mrow / 64) * N;
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int n = cb0 + 32 * ni;
-          if (n < N) {
-            *(v4f*)(prow + n) = v4f{csum[ni][0], csum[ni][1], csum[ni][2], csum[ni][3]};
-            *(v4f*)(prow + n + 4) = v4f{csum[ni][4], csum[ni][5], csum[ni][6], csum[ni][7]};
-          }
-        }
+        for (int v = 0; v < VPL; v += 4) *(v4f*)(prow + v) = v4f{csum[v], csum[v + 1], csum[v + 2], csum[v + 3]};
       }
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) csum[ni][r] = 0.f;
+      for (int v = 0; v < VPL; ++v) csum[v] = 0.f;
     }
   }
 }
@@ -468,6 +496,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
+  char* const scr = smem + TM::LDS_T + wave * EPI_SCR;   // this wave's epilogue scratch
   const int64_t z = GRP ? 0 : blockIdx.z;
 
   // units: standard = output tiles (this block's slice is blockIdx.y);
@@ -738,7 +767,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     if (nt == 0 && wm == 0) SEG_BARRIER();
     STAMP(2);
     if constexpr (BM != 256) {
-      epilogue4<OutT, EPI, F8 != 0, BM>(args, acc, z, m0, n0, wm, wn, lane, sa, sb);
+      epilogue4<OutT, EPI, F8 != 0, BM>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
     } else if (GRP) {
       const WgProb& q = gp->p[u.prob];
       if (u.slot >= 0) {
@@ -753,13 +782,13 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
         ea.ldc = q.K;
         ea.alpha = 1.f;
         ea.beta = gp->beta;
-        epilogue4<OutT, EPI>(ea, acc, 0, m0, n0, wm, wn, lane);
+        epilogue4<OutT, EPI>(ea, acc, 0, m0, n0, wm, wn, lane, scr);
       }
     } else if (SPLIT) {
       epilogue4_slab(args.workspace + ((int64_t)z * args.splitk + blockIdx.y) * args.M * args.N, (int)args.M,
                      (int)args.N, args.alpha, acc, m0, n0, wm, wn, lane);
     } else {
-      epilogue4<OutT, EPI, F8 != 0>(args, acc, z, m0, n0, wm, wn, lane, sa, sb);
+      epilogue4<OutT, EPI, F8 != 0>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
     }
     STAMP(3);
 #ifdef GEMM4_STAMPS
@@ -873,21 +902,21 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   if constexpr (LA == LAY_KC) {
     if (use_bm192(a, ncu)) {
       auto kern = gemm4_kernel<LA, LB, OutT, EPI, false, 192>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_T);
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_ALL);
       const int tiles = (int)((a.M + 191) / 192) * gn;
-      hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_T, s, a);
+      hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_ALL, s, a);
       MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
       return 0;
     }
   }
   const int gm = (int)((a.M + 255) / 256);
   auto kern = S > 1 ? gemm4_kernel<LA, LB, OutT, EPI, true> : gemm4_kernel<LA, LB, OutT, EPI, false>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
   // one block per CU (128 KiB LDS): persistent over tiles for plain launches;
   // split-K / batched launches get one block per (tile, slice, batch)
   const int tiles = gm * gn;
   const int grid = (S * a.batch > 1 || tiles < ncu) ? tiles : ncu;
-  hipLaunchKernelGGL(kern, dim3(grid, S, (unsigned)a.batch), dim3(512), LDS_BYTES, s, a);
+  hipLaunchKernelGGL(kern, dim3(grid, S, (unsigned)a.batch), dim3(512), TileM<256>::LDS_ALL, s, a);
   MC_CHECK_LAUNCH("maeclip_gemm(v4)");
   return 0;
 }
@@ -959,17 +988,17 @@ int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipS
   const int gn = (int)((a.N + 255) / 256);
   if (use_bm192(a, ncu)) {
     auto kern = gemm4_f8_kernel<OutT, EPI, F8, 192>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_T);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_ALL);
     const int tiles = (int)((a.M + 191) / 192) * gn;
-    hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_T, s, g);
+    hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_ALL, s, g);
     MC_CHECK_LAUNCH("maeclip_gemm_fp8(192-row tiles)");
     return 0;
   }
   auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
   const int tiles = (int)(((a.M + 255) / 256) * gn);
   const int grid = (a.batch > 1 || tiles < ncu) ? tiles : ncu;
-  hipLaunchKernelGGL(kern, dim3(grid, 1, (unsigned)a.batch), dim3(512), LDS_BYTES, s, g);
+  hipLaunchKernelGGL(kern, dim3(grid, 1, (unsigned)a.batch), dim3(512), TileM<256>::LDS_ALL, s, g);
   MC_CHECK_LAUNCH("maeclip_gemm_fp8");
   return 0;
 }
@@ -1169,8 +1198,8 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       g.S = 1;
       g.NT = (int)(M / 64);
       g.Tdp = T - T % wg_ncu();
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(wg_ncu()), dim3(512), LDS_BYTES, s, g);
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(wg_ncu()), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k)");
       hipLaunchKernelGGL(wgrad4_sk_reduce_kernel, dim3(T - g.Tdp, SKR_CHUNKS), dim3(256), 0, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k reduce)");
@@ -1186,8 +1215,8 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
     }
     const int units = T * g.S, grid = std::min(units, wg_ncu());
     if (g.S > 1) {
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      hipLaunchKernelGGL(wgrad4_kernel<true>, dim3(grid), dim3(512), LDS_BYTES, s, g);
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      hipLaunchKernelGGL(wgrad4_kernel<true>, dim3(grid), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
       int64_t maxnk = 0;
       for (int i = 0; i < n; ++i) maxnk = std::max(maxnk, (int64_t)g.p[i].N * g.p[i].K);
@@ -1195,8 +1224,8 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       hipLaunchKernelGGL(wgrad4_reduce_kernel, dim3(gx, n), dim3(256), 0, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(reduce)");
     } else {
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(grid), dim3(512), LDS_BYTES, s, g);
+      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(grid), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
     }
   }
