@@ -203,6 +203,13 @@ typedef struct {
   const int64_t* step_ptr; /* optional: both seeds + (*step_ptr) * MAECLIP_STEP_MULT */
   int64_t M, D, ldx, ldy;
   float eps;
+  /* optional fp8 copy of y for an fp8 GEMM (C4): q8 [M, ldq8] quantised per
+   * row exactly as maeclip_quant_rows_fp8 would quantise the stored y (format
+   * q8_fmt, scales q8_scale [M]) -- the quantisation pass fused into the LN */
+  void* q8;
+  int64_t ldq8;
+  float* q8_scale;
+  int32_t q8_fmt;
 } maeclip_ln_fwd_args;
 int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* args, void* stream);
 
@@ -231,6 +238,12 @@ typedef struct {
   int64_t M, D, ldx, lddy, lddx;
   const float* dres_pool;
   int64_t pool_n;
+  /* optional fp8 copy of dx_bf (required with it) for an fp8 dgrad GEMM, as
+   * maeclip_quant_rows_fp8 of dx_bf with format q8_fmt (fused) */
+  void* q8;
+  int64_t ldq8;
+  float* q8_scale;
+  int32_t q8_fmt;
 } maeclip_ln_bwd_args;
 int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* args, void* stream);
 int32_t maeclip_ln_bwd_partial_rows(int64_t M);

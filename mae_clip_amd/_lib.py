@@ -43,7 +43,8 @@ class LnFwdArgs(C.Structure):
                 ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("y_dtype", c_i32), ("y2", c_vp), ("ldy2", c_i64),
                 ("xsum_out", c_vp), ("ldxs", c_i64), ("mean", c_vp), ("rstd", c_vp), ("out_dropout_p", c_f32),
                 ("seed_in", c_u64), ("seed_out", c_u64), ("step_ptr", c_vp),
-                ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("ldy", c_i64), ("eps", c_f32)]
+                ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("ldy", c_i64), ("eps", c_f32),
+                ("q8", c_vp), ("ldq8", c_i64), ("q8_scale", c_vp), ("q8_fmt", c_i32)]
 
 
 class LnBwdArgs(C.Structure):
@@ -52,7 +53,8 @@ class LnBwdArgs(C.Structure):
                 ("dx", c_vp), ("dx_bf", c_vp), ("lddx_bf", c_i64),
                 ("dgamma_partial", c_vp), ("dbeta_partial", c_vp), ("dx_colsum_partial", c_vp),
                 ("M", c_i64), ("D", c_i64), ("ldx", c_i64), ("lddy", c_i64), ("lddx", c_i64),
-                ("dres_pool", c_vp), ("pool_n", c_i64)]
+                ("dres_pool", c_vp), ("pool_n", c_i64),
+                ("q8", c_vp), ("ldq8", c_i64), ("q8_scale", c_vp), ("q8_fmt", c_i32)]
 
 
 class MtEntry(C.Structure):

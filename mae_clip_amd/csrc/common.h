@@ -106,6 +106,23 @@ template <> __device__ __forceinline__ void st4<bf16_t>(bf16_t* p, v4f v) {
   *(v2u*)p = u;
 }
 
+// OCP fp8 (gfx950 v_cvt_pk_fp8_f32 = e4m3fn, v_cvt_pk_bf8_f32 = e5m2, RNE) of
+// four values -> one dword; row quantisation "q = rne(x / s), s = amax / MAX"
+// (fp8.hip, layernorm.hip)
+constexpr float MC_E4M3_MAX = 448.f;
+constexpr float MC_E5M2_MAX = 57344.f;
+template <bool E5> __device__ __forceinline__ unsigned mc_cvt4_fp8(float a, float b, float c, float d) {
+  int r;
+  if (E5) {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  }
+  return (unsigned)r;
+}
+
 // erf-GELU (nn.GELU() / HF "gelu" / timm default) and its derivative sharing
 // one exp: Phi(x) = 0.5 erfc(-x/sqrt2) with erfc by Abramowitz & Stegun 7.1.26
 // (|err| <= 1.5e-7; |gelu err| <= 4.2e-7 over [-12,12], the same as f32 erff),

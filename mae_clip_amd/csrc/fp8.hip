@@ -25,19 +25,11 @@
 
 namespace {
 
-constexpr float E4M3_MAX = 448.f;
-constexpr float E5M2_MAX = 57344.f;
+constexpr float E4M3_MAX = MC_E4M3_MAX;
+constexpr float E5M2_MAX = MC_E5M2_MAX;
 
 template <bool E5> __device__ __forceinline__ unsigned cvt4(float a, float b, float c, float d) {
-  int r;
-  if (E5) {
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
-  } else {
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  }
-  return (unsigned)r;
+  return mc_cvt4_fp8<E5>(a, b, c, d);
 }
 
 template <typename T> struct Row8;   // 8 consecutive elements as f32

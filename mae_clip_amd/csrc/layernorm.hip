@@ -38,6 +38,30 @@ __device__ __forceinline__ void load_row(float (&v)[NC][4], const T* p, int D, i
   }
 }
 
+// the value a consumer reads back from a YT store of f
+template <typename YT> __device__ __forceinline__ float as_stored(float f) {
+  return sizeof(YT) == 2 ? bf2f(f2bf(f)) : f;
+}
+
+// fp8 copy of a row held by one wave (lane: NC chunks of 4 at c * 256 + 4 lane),
+// bit-identical to maeclip_quant_rows_fp8 of the stored row: s = amax / MAX
+// (1 if amax = 0), q = rne(v / s)
+template <int NC>
+__device__ __forceinline__ void quant_row_fp8(const float (&v)[NC][4], float amax, bool e5, uint8_t* q, float* scale,
+                                              int D, int lane) {
+  amax = wave_max(amax);
+  const float s = amax > 0.f ? amax / (e5 ? MC_E5M2_MAX : MC_E4M3_MAX) : 1.f;
+  const float inv = 1.f / s;
+  if (lane == 0) *scale = s;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e = c * 256 + lane * 4;
+    if (e < D)
+      *(unsigned*)(q + e) = e5 ? mc_cvt4_fp8<true>(v[c][0] * inv, v[c][1] * inv, v[c][2] * inv, v[c][3] * inv)
+                               : mc_cvt4_fp8<false>(v[c][0] * inv, v[c][1] * inv, v[c][2] * inv, v[c][3] * inv);
+  }
+}
+
 __device__ __forceinline__ float keepf(uint64_t seed, int64_t row, int col, uint32_t thr, float sc) {
   return mc_hash4(seed, (uint64_t)row, (uint64_t)col, 0x4c4eull) >= thr ? sc : 0.f;
 }
@@ -88,6 +112,7 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
   const bool odrop = a.out_dropout_p > 0.f;
   const uint32_t othr = (uint32_t)((double)a.out_dropout_p * 4294967296.0);
   const float osc = odrop ? 1.f / (1.f - a.out_dropout_p) : 1.f;
+  float amax = 0.f;   // of the stored y (fp8 copy only)
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int e = c * 256 + lane * 4;
@@ -100,10 +125,13 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
     for (int j = 0; j < 4; ++j) {
       y[j] = (v[c][j] - mean) * rstd * gm[j] + bt[j];
       if (odrop) y[j] *= keepf(mc_step_seed(a.seed_out, a.step_ptr), row, e + j, othr, osc);
+      v[c][j] = as_stored<YT>(y[j]);
+      amax = fmaxf(amax, fabsf(v[c][j]));
     }
     st4<YT>((YT*)a.y + row * a.ldy + e, y);
     if (a.y2) st4<bf16_t>((bf16_t*)a.y2 + row * a.ldy2 + e, y);
   }
+  if (a.q8) quant_row_fp8<NC>(v, amax, a.q8_fmt == MAECLIP_FP8_E5M2, (uint8_t*)a.q8 + row * a.ldq8, a.q8_scale + row, D, lane);
 }
 
 template <int NC, typename GT, typename XT>
@@ -152,6 +180,7 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
       }
     s1 = wave_sum(s1) / D;
     s2 = wave_sum(s2) / D;
+    float amax = 0.f;   // of the bf16 dx copy (fp8 copy only)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int e = c * 256 + lane * 4;
@@ -163,10 +192,13 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
         if (a.dres || pool) d += dr[c][j];
         o[j] = d;
         pc[c][j] += d;
+        dy[c][j] = as_stored<bf16_t>(d);
+        amax = fmaxf(amax, fabsf(dy[c][j]));
       }
       *(v4f*)(a.dx + row * a.lddx + e) = o;
       if (a.dx_bf) st4<bf16_t>((bf16_t*)a.dx_bf + row * a.lddx_bf + e, o);
     }
+    if (a.q8) quant_row_fp8<NC>(dy, amax, a.q8_fmt == MAECLIP_FP8_E5M2, (uint8_t*)a.q8 + row * a.ldq8, a.q8_scale + row, D, lane);
   }
   // cross-wave reduction of the three per-lane partial vectors
   float* outs[3] = {a.dgamma_partial, a.dbeta_partial, a.dx_colsum_partial};
@@ -201,6 +233,9 @@ int ln_bwd_grid(int64_t M) {
 extern "C" int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* a, void* stream) {
   MC_CHECK_ARG(a && a->x && a->y && a->gamma && a->beta, "maeclip_ln_fwd: null pointer");
   MC_CHECK_ARG(a->D > 0 && a->D <= MAXC * 256 && a->D % 4 == 0, "maeclip_ln_fwd: D=%lld unsupported", (long long)a->D);
+  MC_CHECK_ARG(!a->q8 || (a->q8_scale && a->ldq8 >= a->D && a->ldq8 % 4 == 0 && ((uintptr_t)a->q8 & 3) == 0 &&
+                          (a->q8_fmt == MAECLIP_FP8_E4M3 || a->q8_fmt == MAECLIP_FP8_E5M2)),
+               "maeclip_ln_fwd: bad fp8 output");
   if (a->M == 0) return 0;
   dim3 grid((unsigned)((a->M + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
@@ -224,6 +259,9 @@ extern "C" int32_t maeclip_ln_bwd_partial_rows(int64_t M) { return ln_bwd_grid(M
 extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
   MC_CHECK_ARG(a && a->dy && a->x && a->mean && a->rstd && a->gamma && a->dx, "maeclip_ln_bwd: null pointer");
   MC_CHECK_ARG(a->D > 0 && a->D <= MAXC * 256 && a->D % 4 == 0, "maeclip_ln_bwd: D unsupported");
+  MC_CHECK_ARG(!a->q8 || (a->dx_bf && a->q8_scale && a->ldq8 >= a->D && a->ldq8 % 4 == 0 && ((uintptr_t)a->q8 & 3) == 0 &&
+                          (a->q8_fmt == MAECLIP_FP8_E4M3 || a->q8_fmt == MAECLIP_FP8_E5M2)),
+               "maeclip_ln_bwd: bad fp8 output (needs dx_bf)");
   MC_CHECK_ARG(!a->dres_pool || (!a->dres && a->pool_n > 1 && a->M % a->pool_n == 0),
                "maeclip_ln_bwd: dres_pool needs pool_n > 1 dividing M (and no dres)");
   if (a->M == 0) return 0;

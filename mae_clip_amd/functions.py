@@ -144,22 +144,29 @@ class StackSpec:
     w8: list = None                 # fp8 mode: per block ((W, W^T) fp8 operands) x (qkv, proj, fc1, fc2)
 
 
-def _fwd(x, w, w8, **kw):
+def _fwd(x, w, w8, xq=None, **kw):
     """Forward GEMM of a stack: bf16 / fp32 (w), or fp8 (w8 = (W, W^T)): x is
-    quantised per token (e4m3) and multiplied with W (per output channel)."""
+    quantised per token (e4m3; xq: already quantised by its producer, the
+    LayerNorm) and multiplied with W (per output channel)."""
     if w8 is None:
         return K.linear_fwd(x, w, **kw)
     kw.setdefault("out_dtype", x.dtype)
-    return K.linear_fp8(K.quant_rows_fp8(x, K.FP8_E4M3), w8[0], **kw)
+    return K.linear_fp8(xq if xq is not None else K.quant_rows_fp8(x, K.FP8_E4M3), w8[0], **kw)
 
 
-def _dgrad(dy, w, w8, **kw):
+def _dgrad(dy, w, w8, dyq=None, **kw):
     """dgrad GEMM dX = dY W: fp8 mode quantises dY per token (e5m2, the wider
-    range of gradients) and multiplies with W^T (per input channel)."""
+    range of gradients; dyq: already quantised by the LayerNorm backward) and
+    multiplies with W^T (per input channel)."""
     if w8 is None:
         return K.linear_dgrad(dy, w, **kw)
     kw.setdefault("out_dtype", dy.dtype)
-    return K.linear_fp8(K.quant_rows_fp8(dy, K.FP8_E5M2), w8[1], **kw)
+    return K.linear_fp8(dyq if dyq is not None else K.quant_rows_fp8(dy, K.FP8_E5M2), w8[1], **kw)
+
+
+def _q8(f8, M, D, fmt, dev):
+    """Fp8Rows for a LayerNorm to fill when its consumer GEMM runs in fp8."""
+    return K.new_fp8_rows(M, D, fmt, dev) if f8 is not None else None
 
 
 PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
@@ -179,14 +186,18 @@ class TransformerStackFn(torch.autograd.Function):
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
             f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
-            h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T)
-            qkv = _fwd(h1, wqkv, f8[0], bias=bqkv)
+            q1 = _q8(f8[0], M, D, K.FP8_E4M3, x.device)
+            h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T, q8=q1)
+            qkv = _fwd(h1, wqkv, f8[0], xq=q1, bias=bqkv)
+            del q1
             o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
             x1 = _fwd(o, wproj, f8[1], bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
-            h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T)
+            q2 = _q8(f8[2], M, D, K.FP8_E4M3, x.device)
+            h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T, q8=q2)
             # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
             dgelu = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
-            a = _fwd(h2, w1, f8[2], bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
+            a = _fwd(h2, w1, f8[2], xq=q2, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
+            del q2
             x2 = _fwd(a, w2, f8[3], bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
             saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a])
             xi = x2
@@ -216,6 +227,7 @@ class TransformerStackFn(torch.autograd.Function):
         cpart = K.rows_colsum(g, out_bf16=gT)
         if not bf:
             gT = g
+        gq = None   # fp8 (e5m2) copy of gT made by the LayerNorm backward that produced it
         for i in reversed(range(len(spec.wT))):
             wqkv, wproj, w1, w2 = spec.wT[i]
             f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
@@ -227,7 +239,8 @@ class TransformerStackFn(torch.autograd.Function):
             # mlp.fc2 (+ GELU backward fused into the dgrad epilogue: dA = (dy W2) * gelu'(h))
             gi[11] = rb.add(cpart, out=gout(ar, p[11]))
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
-            dA = _dgrad(gT, w2, f8[3], epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
+            dA = _dgrad(gT, w2, f8[3], dyq=gq, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
+            gq = None
             gi[10] = wq.wgrad(gT, a, out=gout(ar, p[10]))
             del a, dgelu
             # mlp.fc1
@@ -236,13 +249,15 @@ class TransformerStackFn(torch.autograd.Function):
             gi[8] = wq.wgrad(dA, h2, out=gout(ar, p[8]))
             del dA
             # norm2 (+ residual gradient)
-            dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True)
+            q1 = _q8(f8[1], M, D, K.FP8_E5M2, g.device) if bf else None
+            dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True, q8=q1)
             gi[6], gi[7] = rb.add(pg, out=gout(ar, p[6])), rb.add(pb, out=gout(ar, p[7]))
             if not bf:
                 dx1T = dx1
             # attn.proj
             gi[5] = rb.add(pc, out=gout(ar, p[5]))
-            dO = _dgrad(dx1T, wproj, f8[1])
+            dO = _dgrad(dx1T, wproj, f8[1], dyq=q1)
+            del q1
             gi[4] = wq.wgrad(dx1T, o, out=gout(ar, p[4]))
             # attention
             dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
@@ -252,7 +267,10 @@ class TransformerStackFn(torch.autograd.Function):
             gi[2] = wq.wgrad(dqkv, h1, out=gout(ar, p[2]))
             del dqkv
             # norm1 (+ residual gradient)
-            dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True)
+            # the next (lower) block's fc2 dgrad reads dxT: quantised here when it is fp8
+            f8n = (spec.w8[i - 1][3] if spec.w8 is not None and i > 0 else None)
+            gq = _q8(f8n, M, D, K.FP8_E5M2, g.device) if bf else None
+            dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True, q8=gq)
             gi[0], gi[1] = rb.add(pg, out=gout(ar, p[0])), rb.add(pb, out=gout(ar, p[1]))
             ctx.saved[i] = None
             g, gT, cpart = dx, (dxT if bf else dx), pc

@@ -102,6 +102,12 @@ class Fp8Rows:
         return self.q.shape
 
 
+def new_fp8_rows(rows, cols, fmt, device):
+    """An empty Fp8Rows to be filled by a producer kernel (ln_fwd / ln_bwd q8=)."""
+    return Fp8Rows(torch.empty((rows, cols), device=device, dtype=torch.uint8),
+                   torch.empty((rows,), device=device, dtype=torch.float32), fmt)
+
+
 def quant_rows_fp8(x, fmt=FP8_E4M3, out=None):
     """Row-wise fp8 quantisation of x [rows, cols] (bf16 / f32): one pass,
     s = amax(row) / FMT_MAX."""
@@ -333,8 +339,9 @@ def embed_fwd(ids, word, pos):
 
 # -------------------------------------------------------------- LayerNorm
 def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dropout=0.0, seed_in=0, seed_out=0,
-           want_stats=True, y2=False, xsum=False, step_ptr=None):
-    """Returns (y, mean, rstd, y2_bf16, xsum)."""
+           want_stats=True, y2=False, xsum=False, step_ptr=None, q8=None):
+    """Returns (y, mean, rstd, y2_bf16, xsum). q8 (Fp8Rows, optional): also
+    filled with the fp8 row quantisation of y (== quant_rows_fp8(y, q8.fmt))."""
     _dev(x, gamma, beta, res)
     M, D = x.shape
     dev = x.device
@@ -348,6 +355,8 @@ def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dr
                     y_dtype=_dt(y), y2=_ptr(yb), ldy2=D, xsum_out=_ptr(xs), ldxs=D, mean=_ptr(mean), rstd=_ptr(rstd),
                     out_dropout_p=out_dropout, seed_in=int(seed_in), seed_out=int(seed_out), step_ptr=_ptr(step_ptr),
                     M=M, D=D, ldx=x.stride(0), ldy=D, eps=eps)
+    if q8 is not None:
+        a.q8, a.ldq8, a.q8_scale, a.q8_fmt = q8.q.data_ptr(), q8.q.stride(0), q8.s.data_ptr(), q8.fmt
     _call("maeclip_ln_fwd", C.byref(a), _stream())
     return y, mean, rstd, yb, xs
 
@@ -357,8 +366,9 @@ def ln_bwd_partial_rows(M: int) -> int:
 
 
 def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False,
-           dres_pool=None, pool_n=0):
+           dres_pool=None, pool_n=0, q8=None):
     """Returns (dx f32, dx_bf16, dgamma_partial, dbeta_partial, dx_colsum_partial).
+    q8 (Fp8Rows, with want_bf16): also filled with quant_rows_fp8(dx_bf16, q8.fmt).
     dres_pool [M / pool_n, D]: residual gradient = the avg-pool backward of it
     (1/(pool_n-1) on every non-cls row), fused instead of a dres tensor."""
     _dev(dy, x, mean, rstd, gamma, dres, dres_pool)
@@ -375,6 +385,8 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
                     lddx_bf=D, dgamma_partial=_ptr(pg), dbeta_partial=_ptr(pb), dx_colsum_partial=_ptr(pc),
                     M=M, D=D, ldx=x.stride(0), lddy=dy.stride(0), lddx=D, dres_pool=_ptr(dres_pool),
                     pool_n=int(pool_n))
+    if q8 is not None:
+        a.q8, a.ldq8, a.q8_scale, a.q8_fmt = q8.q.data_ptr(), q8.q.stride(0), q8.s.data_ptr(), q8.fmt
     _call("maeclip_ln_bwd", C.byref(a), _stream())
     return dx, dxb, pg, pb, pc
 

@@ -41,6 +41,30 @@ def test_quant_rows_bit_exact(dev, fmt, dtype, cols):
     assert torch.equal(out.q.cpu(), q_ref.view(torch.uint8))
 
 
+@pytest.mark.parametrize("D", [512, 768, 1024])
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+def test_layernorm_fused_fp8_copy_bit_exact(dev, D, fmt):
+    """The LayerNorm forward / backward fill the fp8 operand of the next GEMM
+    themselves (the quantisation pass fused): identical bytes and scales to
+    quant_rows_fp8 of the bf16 output they store (y; the dx copy)."""
+    M = 300
+    g = torch.Generator().manual_seed(D + fmt)
+    x = (torch.randn(M, D, generator=g) * 3 + 1).to(dev)
+    x[4] = 0.0                                         # constant row: y = beta
+    gam = (torch.rand(D, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(D, generator=g) * 0.1).to(dev)
+    q = K.new_fp8_rows(M, D, fmt, x.device)
+    y, mean, rstd, _, _ = K.ln_fwd(x, gam, bet, 1e-6, out_dtype=torch.bfloat16, q8=q)
+    r = K.quant_rows_fp8(y, fmt)
+    assert torch.equal(q.s, r.s) and torch.equal(q.q, r.q)
+    dy = (torch.randn(M, D, generator=g) * 1e-3).to(torch.bfloat16).to(dev)
+    dres = (torch.randn(M, D, generator=g) * 1e-3).to(dev)
+    qb = K.new_fp8_rows(M, D, fmt, x.device)
+    dx, dxb, _, _, _ = K.ln_bwd(dy, x, mean, rstd, gam, dres=dres, want_bf16=True, q8=qb)
+    rb = K.quant_rows_fp8(dxb, fmt)
+    assert torch.equal(qb.s, rb.s) and torch.equal(qb.q, rb.q)
+
+
 def test_quant_cols_bit_exact(dev):
     g = torch.Generator().manual_seed(7)
     w = (torch.randn(200, 136, generator=g) * torch.logspace(-3, 1, 136)).to(dev)
