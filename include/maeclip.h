@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 4
+#define MAECLIP_ABI_VERSION 5
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
