@@ -155,8 +155,12 @@ int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int32_t nprob,
  * (modeling_distilbert.py:125-145). qkv: [B*n, ld_qkv] token rows with q at
  * column h*hd, k at H*hd + h*hd, v at 2*H*hd + h*hd. o: [B*n, ld_o].
  * lse: [B, H, n] f32, log2-domain row log-sum-exp of scale*q.k (bwd input).
- * key_mask (optional, f32 [B, n]): 0 = padding key. dropout_p applies to the
- * probabilities in the forward only (DistilBERT attention dropout; no bwd).
+ * key_mask (optional, f32 [B, n]): 0 = padding key (forward; the backward
+ * takes it only in fp32 at n beyond the LDS images -- the streamed "rows"
+ * path -- and rejects it otherwise: the frozen text tower has no backward).
+ * dropout_p applies to the probabilities in the forward only (DistilBERT
+ * attention dropout; no bwd). fp32 forward / backward at any n: past the LDS
+ * images (n ~ 540 at hd 32) 64-row blocks are streamed (no dropout there).
  * bwd: dout [B*n, ld_o], dqkv [B*n, ld_dqkv]; colsum_partial optional
  * [B, 3*H*hd] per-sample column sums of dqkv (qkv bias gradient). */
 typedef struct {

@@ -1005,6 +1005,213 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   ASTAMP(5);
 }
 
+// ============================================ fp32 parity mode, long sequences
+// The fp32 images of the MFMA kernels take 2 npad (4 HD + 16) bytes of LDS (the
+// forward's K / V, the backward's two-image slots): past n ~ 540 at HD = 32 --
+// the C4 decoder, n = 577 -- they do not fit in 160 KiB. These kernels stream
+// 64-row blocks of the other side through LDS instead: one thread per query
+// (forward, dQ) or key (dK, dV) row, exact f32 FMA, and the conventions of the
+// MFMA kernels (scores in log2 units, lse2 = m + log2 l, Dv = -rowsum(dO O),
+// dS = P (dP + Dv), the bias partials' zero k slice), so both agree to f32
+// rounding. Parity mode only: the bf16 path never comes here.
+constexpr int RB = 64;   // rows per streamed block = threads per workgroup
+
+template <int HD>
+__device__ __forceinline__ void load_row(float (&r)[HD], const float* p, bool ok) {
+#pragma unroll
+  for (int d = 0; d < HD; d += 4) {
+    const v4f v = ok ? *(const v4f*)(p + d) : v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[d + j] = v[j];
+  }
+}
+template <int HD>
+__device__ __forceinline__ float dot_row(const float (&r)[HD], const float* l) {
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) s = fmaf(r[d], l[d], s);
+  return s;
+}
+// rows r0 .. r0 + RB - 1 of one head slice -> LDS [RB][HD] (zero past n)
+template <int HD>
+__device__ __forceinline__ void stage_rows(float (*dst)[HD], const float* src, int64_t ld, int r0, int n) {
+  for (int i = threadIdx.x; i < RB * HD / 4; i += RB) {
+    const int r = i / (HD / 4), c = 4 * (i % (HD / 4));
+    *(v4f*)&dst[r][c] = r0 + r < n ? *(const v4f*)(src + (int64_t)(r0 + r) * ld + c) : v4f{0.f, 0.f, 0.f, 0.f};
+  }
+}
+__device__ __forceinline__ float key_bias(const maeclip_attn_args& a, int b, int k) {
+  return k < a.n && !(a.key_mask && a.key_mask[(int64_t)b * a.n + k] == 0.f) ? 0.f : NEG_BIG;
+}
+
+template <int HD>
+__global__ void __launch_bounds__(RB) attn_fwd_rows_kernel(const maeclip_attn_args a) {
+  __shared__ __attribute__((aligned(16))) float Kb[RB][HD], Vb[RB][HD];
+  __shared__ float mb[RB];
+  const int n = a.n, H = a.H, HH = H * HD;
+  const int b = blockIdx.y / H, h = blockIdx.y % H;
+  const int q = blockIdx.x * RB + threadIdx.x;
+  const bool qok = q < n;
+  const float* qkv = (const float*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  float qv[HD], o[HD];
+  load_row<HD>(qv, qkv + (int64_t)(qok ? q : 0) * a.ld_qkv + h * HD, qok);
+#pragma unroll
+  for (int d = 0; d < HD; ++d) o[d] = 0.f;
+  const float c = a.scale * LOG2E;
+  float m = NEG_BIG, l = 0.f;
+  for (int k0 = 0; k0 < n; k0 += RB) {
+    __syncthreads();
+    stage_rows<HD>(Kb, qkv + HH + h * HD, a.ld_qkv, k0, n);
+    stage_rows<HD>(Vb, qkv + 2 * HH + h * HD, a.ld_qkv, k0, n);
+    mb[threadIdx.x] = key_bias(a, b, k0 + threadIdx.x);
+    __syncthreads();
+    const int kn = min(RB, n - k0);
+    for (int j = 0; j < kn; ++j) {
+      const float s = fmaf(dot_row<HD>(qv, Kb[j]), c, mb[j]);
+      const float mn = fmaxf(m, s);
+      const float corr = __builtin_amdgcn_exp2f(m - mn), p = __builtin_amdgcn_exp2f(s - mn);
+      l = fmaf(l, corr, p);
+#pragma unroll
+      for (int d = 0; d < HD; ++d) o[d] = fmaf(o[d], corr, p * Vb[j][d]);
+      m = mn;
+    }
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    float* orow = (float*)a.o + ((int64_t)b * n + q) * a.ld_o + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) *(v4f*)(orow + d) = v4f{o[d], o[d + 1], o[d + 2], o[d + 3]} * inv;
+    if (a.lse) a.lse[((int64_t)b * H + h) * n + q] = m + log2f(l);
+  }
+}
+
+// dQ: one thread per query row, 64-key blocks of K, V through LDS
+template <int HD>
+__global__ void __launch_bounds__(RB) attn_bwd_rows_dq_kernel(const maeclip_attn_args a) {
+  __shared__ __attribute__((aligned(16))) float Kb[RB][HD], Vb[RB][HD];
+  __shared__ float mb[RB];
+  const int n = a.n, H = a.H, HH = H * HD;
+  const int b = blockIdx.y / H, h = blockIdx.y % H;
+  const int q = blockIdx.x * RB + threadIdx.x;
+  const bool qok = q < n;
+  const int qr = qok ? q : 0;
+  const float* qkv = (const float*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  float qv[HD], dov[HD], dq[HD];
+  load_row<HD>(qv, qkv + (int64_t)qr * a.ld_qkv + h * HD, qok);
+  load_row<HD>(dov, (const float*)a.dout + ((int64_t)b * n + qr) * a.ld_o + h * HD, qok);
+  const float Dq = -dot_row<HD>(dov, (const float*)a.o + ((int64_t)b * n + qr) * a.ld_o + h * HD);
+  const float L = qok ? a.lse[((int64_t)b * H + h) * n + q] : 1.0e30f;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) dq[d] = 0.f;
+  const float c = a.scale * LOG2E;
+  for (int k0 = 0; k0 < n; k0 += RB) {
+    __syncthreads();
+    stage_rows<HD>(Kb, qkv + HH + h * HD, a.ld_qkv, k0, n);
+    stage_rows<HD>(Vb, qkv + 2 * HH + h * HD, a.ld_qkv, k0, n);
+    mb[threadIdx.x] = key_bias(a, b, k0 + threadIdx.x);
+    __syncthreads();
+    const int kn = min(RB, n - k0);
+    for (int j = 0; j < kn; ++j) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(dot_row<HD>(qv, Kb[j]), c, mb[j]) - L);
+      const float ds = p * (dot_row<HD>(dov, Vb[j]) + Dq);
+#pragma unroll
+      for (int d = 0; d < HD; ++d) dq[d] = fmaf(ds, Kb[j][d], dq[d]);
+    }
+  }
+  if (qok) {
+    float* row = (float*)a.dqkv + ((int64_t)b * n + q) * a.ld_dqkv + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) *(v4f*)(row + d) = v4f{dq[d], dq[d + 1], dq[d + 2], dq[d + 3]} * a.scale;
+  }
+}
+
+// dK, dV: one thread per key row, 64-query blocks of Q, dO (+ lse2, Dv) through LDS
+template <int HD>
+__global__ void __launch_bounds__(RB) attn_bwd_rows_dkv_kernel(const maeclip_attn_args a) {
+  __shared__ __attribute__((aligned(16))) float Qb[RB][HD], Db[RB][HD];
+  __shared__ float Lb[RB], Dvb[RB];
+  const int n = a.n, H = a.H, HH = H * HD;
+  const int b = blockIdx.y / H, h = blockIdx.y % H;
+  const int k = blockIdx.x * RB + threadIdx.x;
+  const bool kok = k < n;
+  const int kr = kok ? k : 0;
+  const float* qkv = (const float*)a.qkv + (int64_t)b * n * a.ld_qkv;
+  const float* O = (const float*)a.o + (int64_t)b * n * a.ld_o + h * HD;
+  const float* dO = (const float*)a.dout + (int64_t)b * n * a.ld_o + h * HD;
+  float kv[HD], vv[HD], dk[HD], dv[HD];
+  load_row<HD>(kv, qkv + (int64_t)kr * a.ld_qkv + HH + h * HD, kok);
+  load_row<HD>(vv, qkv + (int64_t)kr * a.ld_qkv + 2 * HH + h * HD, kok);
+  const float mk = key_bias(a, b, k);
+#pragma unroll
+  for (int d = 0; d < HD; ++d) dk[d] = dv[d] = 0.f;
+  const float c = a.scale * LOG2E;
+  for (int q0 = 0; q0 < n; q0 += RB) {
+    __syncthreads();
+    stage_rows<HD>(Qb, qkv + h * HD, a.ld_qkv, q0, n);
+    stage_rows<HD>(Db, dO, a.ld_o, q0, n);
+    {
+      const int q = q0 + threadIdx.x;
+      const bool ok = q < n;
+      float dr[HD];
+      load_row<HD>(dr, dO + (int64_t)(ok ? q : 0) * a.ld_o, ok);
+      Dvb[threadIdx.x] = ok ? -dot_row<HD>(dr, O + (int64_t)q * a.ld_o) : 0.f;
+      Lb[threadIdx.x] = ok ? a.lse[((int64_t)b * H + h) * n + q] : 1.0e30f;
+    }
+    __syncthreads();
+    const int qn = min(RB, n - q0);
+    for (int j = 0; j < qn; ++j) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(dot_row<HD>(kv, Qb[j]), c, mk) - Lb[j]);
+      const float ds = p * (dot_row<HD>(vv, Db[j]) + Dvb[j]);
+#pragma unroll
+      for (int d = 0; d < HD; ++d) {
+        dv[d] = fmaf(p, Db[j][d], dv[d]);
+        dk[d] = fmaf(ds, Qb[j][d], dk[d]);
+      }
+    }
+  }
+  if (kok) {
+    float* row = (float*)a.dqkv + ((int64_t)b * n + k) * a.ld_dqkv + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD; d += 4) {
+      *(v4f*)(row + HH + d) = v4f{dk[d], dk[d + 1], dk[d + 2], dk[d + 3]} * a.scale;
+      *(v4f*)(row + 2 * HH + d) = v4f{dv[d], dv[d + 1], dv[d + 2], dv[d + 3]};
+    }
+  }
+}
+
+// bias partials of the rows path: column sums of this sample's dqkv rows (the
+// q and v slices of every head; the k slice is identically zero, as above)
+__global__ void __launch_bounds__(256) attn_rows_colsum_kernel(const maeclip_attn_args a, int HH) {
+  const int b = blockIdx.y, col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= 3 * HH) return;
+  float s = 0.f;
+  if (col < HH || col >= 2 * HH) {
+    const float* p = (const float*)a.dqkv + (int64_t)b * a.n * a.ld_dqkv + col;
+    for (int r = 0; r < a.n; ++r) s += p[(int64_t)r * a.ld_dqkv];
+  }
+  a.colsum_partial[(int64_t)b * 3 * HH + col] = s;
+}
+
+template <int HD>
+int run_rows(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
+  MC_CHECK_ARG(bwd || a.dropout_p == 0.f, "maeclip_attn_fwd: the fp32 long-sequence path has no attention dropout");
+  const dim3 grid((unsigned)((a.n + RB - 1) / RB), (unsigned)(a.B * a.H));
+  if (!bwd) {
+    hipLaunchKernelGGL(attn_fwd_rows_kernel<HD>, grid, dim3(RB), 0, s, a);
+    MC_CHECK_LAUNCH("maeclip_attn_fwd(f32 rows)");
+    return 0;
+  }
+  hipLaunchKernelGGL(attn_bwd_rows_dq_kernel<HD>, grid, dim3(RB), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_rows_dkv_kernel<HD>, grid, dim3(RB), 0, s, a);
+  if (a.colsum_partial) {
+    const int HH = a.H * HD;
+    hipLaunchKernelGGL(attn_rows_colsum_kernel, dim3((unsigned)((3 * HH + 255) / 256), (unsigned)a.B), dim3(256), 0,
+                       s, a, HH);
+  }
+  MC_CHECK_LAUNCH("maeclip_attn_bwd(f32 rows)");
+  return 0;
+}
+
 size_t bwd_diag_lds(int n) {
   const int npad = (n + 31) & ~31, nw = npad / 32;
   return (size_t)2 * npad * Img<bf16_t, DIAG_HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 128 +
@@ -1081,7 +1288,12 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
       if (two) lds = lds2;
     }
   }
+  if constexpr (!std::is_same<T, bf16_t>::value) {
+    // fp32 beyond the LDS images (MAECLIP_ATTN_ROWS=1 forces it: tests)
+    if (lds > 163840 || getenv_flag("MAECLIP_ATTN_ROWS")) return run_rows<HD>(a, bwd, s);
+  }
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
+  MC_CHECK_ARG(!bwd || !a.key_mask, "maeclip_attn_bwd: key_mask is supported by the fp32 rows path only");
   dim3 grid((unsigned)(a.B * a.H));
   if constexpr (std::is_same<T, bf16_t>::value && HD == DIAG_HD) {
     // one-pass diagonal backward (MAECLIP_ATTN_DIAG=0 turns it off)

@@ -16,10 +16,15 @@
 //             workspace (3 N^2 f32: 0.8 MB at N = 256, 48 MB at N = 2048), and
 //             the online (max, sumexp) over the workgroup's j range of the rows
 //             of S, L and L^T (a row of L^T = a column of L) -> part1.
-//   stats:    per row i: lse of S / L / L^T rows (part1 combined), c_i =
+//   stats:    per row i: (max M, log sumexp z) of S / L / L^T rows (part1
+//             combined; kept apart, x - lse is taken as (x - M) - z), c_i =
 //             sum_j exp(S_ij - lseS_j) (S symmetric: the column sums of Y) and
-//             rl_i = -(sum_j Y_ij (2 L_ij - lse_col(L)_j) - lse_row(L)_i) / 2N,
-//             one pass over the stored S / L rows -> stat[5][N].
+//             rl_i = -sum_j Y_ij ((L_ij - lse_row(L)_i) + (L_ij - lse_col(L)_j)) / 2N
+//             (log-probabilities as differences: 2 L - lse - lse, or an lse
+//             rounded to f32, loses ~1e-6 absolute at |L| ~ 30, which the nearly
+//             cancelling G - rl and P_r - 2Y + P_c c then amplify: a 16x larger
+//             error than torch's f32 autograd at ViT-L C4 shapes, B = 2),
+//             one pass over the stored S / L rows -> stat[8][N].
 //   grad:     workgroup (16 gradient rows, 16 columns of P): wave w takes the
 //             j-tiles w, w + 4, ...; per tile Dm, dL, dL^T from the stored
 //             tiles and stat, then dI^T / dT^T += X_j^T (.) on the MFMA; the
@@ -51,7 +56,7 @@ struct ClipK {
   int nrep, Js;        // products: j-tiles per workgroup, number of j-splits
   float tau;
   float* part1;        // [Js][3][N] (max, sumexp)
-  float* stat;         // [5][N]: lse of S rows, L rows, L^T rows; c; rl
+  float* stat;         // [8][N]: (max, log sumexp) of S rows, L rows, L^T rows; c; rl
   float* Sm;           // [N][NP] S = (I I^T + T T^T) tau / 2
   float* Lm;           // [N][NP] L = T I^T / tau
   float* Ltm;          // [N][NP] L^T
@@ -66,10 +71,14 @@ __device__ __forceinline__ void merge_ms(float& m, float& s, float m2, float s2)
   m = M;
 }
 
-// lse from partials [js * stride + idx] (max, sumexp pairs), js < n, read 16
-// at a time with every load in flight
-__device__ __forceinline__ float lse_of(const float* part, int64_t stride, int64_t idx, int n) {
-  float M = NEG, z = 0.f;
+// (max, log sumexp) from partials [js * stride + idx] (max, sumexp pairs), js <
+// n, read 16 at a time with every load in flight. The two parts stay separate:
+// lse = M + log z rounded to f32 is off by up to ulp(|M|) / 2 (1e-6 at |x| ~ 30),
+// which the nearly cancelling gradient terms then amplify; x - lse is taken as
+// (x - M) - log z, both exact or small where it matters.
+__device__ __forceinline__ void lse_parts(const float* part, int64_t stride, int64_t idx, int n, float& M, float& lz) {
+  M = NEG;
+  float z = 0.f;
   for (int s0 = 0; s0 < n; s0 += 16) {
     v2f v[16];
 #pragma unroll
@@ -78,8 +87,9 @@ __device__ __forceinline__ float lse_of(const float* part, int64_t stride, int64
 #pragma unroll
     for (int u = 0; u < 16; ++u) merge_ms(M, z, v[u][0], v[u][1]);
   }
-  return M + logf(z);
+  lz = logf(z);
 }
+__device__ __forceinline__ float lsub(float x, float M, float lz) { return (x - M) - lz; }
 
 // i-side B operand of wave role ty: rows i0 + (lane&15), 16-B vector b at k = 16b + 4(lane>>4)
 template <int NB>
@@ -208,64 +218,73 @@ __global__ void __launch_bounds__(NT) clip_products_kernel(const ClipK a) {
 
 // ------------------------------------------------------------------ stats
 // Workgroup = 8 rows; wave w takes rows 2w, 2w + 1 over all j (lane: 4
-// consecutive j per 16-B load). Every workgroup first combines part1 into the
-// lse of S rows and of L^T rows (= L columns) for all j (LDS).
+// consecutive j per 16-B load), j in chunks of JC whose column statistics (S
+// rows = Y columns by symmetry, L columns) the workgroup first combines from
+// part1 into LDS.
+constexpr int JC = 2048;
 __global__ void __launch_bounds__(NT) clip_stats_kernel(const ClipK a) {
-  extern __shared__ __attribute__((aligned(16))) float jl2[];   // [2][NP]
+  __shared__ float jm[4][JC];   // (M, log z) of S rows and of L columns, j of the chunk
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = a.N, NP = a.NP;
   const float inv2n = 0.5f / (float)N;
-  for (int t = threadIdx.x; t < 2 * NP; t += NT) {
-    const int j = t % NP, which = t / NP;
-    jl2[t] = j < N ? lse_of(a.part1, 3LL * N, (which ? 2LL * N : 0LL) + j, a.Js) : 0.f;
-  }
-  __syncthreads();
-  const float* lseS = jl2;
-  const float* lseC = jl2 + NP;
   const int i0 = 8 * (int)blockIdx.x + 2 * w;
-  float lsi[2], lri[2];
+  float ms[2], zs[2], mr[2], zr[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int i = min(i0 + u, N - 1);
-    lsi[u] = lseS[i];
-    lri[u] = lse_of(a.part1, 3LL * N, (int64_t)N + i, a.Js);
+    lse_parts(a.part1, 3LL * N, i, a.Js, ms[u], zs[u]);
+    lse_parts(a.part1, 3LL * N, (int64_t)N + i, a.Js, mr[u], zr[u]);
   }
   float c[2] = {0.f, 0.f}, q[2] = {0.f, 0.f};
-  for (int jb = 4 * lane; jb < N; jb += 512) {
-    v4f Sv[2][2], Lv[2][2];
+  for (int jc0 = 0; jc0 < N; jc0 += JC) {
+    const int jn = min(JC, N - jc0);
+    __syncthreads();   // the previous chunk's reads are done
+    for (int t = threadIdx.x; t < 2 * JC; t += NT) {
+      const int j = t % JC, which = t / JC;
+      float M = 0.f, lz = 0.f;
+      if (j < jn) lse_parts(a.part1, 3LL * N, (which ? 2LL * N : 0LL) + jc0 + j, a.Js, M, lz);
+      jm[2 * which][j] = M;
+      jm[2 * which + 1][j] = lz;
+    }
+    __syncthreads();
+    for (int jb = 4 * lane; jb < jn; jb += 512) {
+      v4f Sv[2][2], Lv[2][2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t o = (int64_t)min(i0 + u, N - 1) * NP + min(jb + 256 * h, NP - 4);
-        Sv[u][h] = *(const v4f*)(a.Sm + o);
-        Lv[u][h] = *(const v4f*)(a.Lm + o);
-      }
+        for (int h = 0; h < 2; ++h) {
+          const int64_t o = (int64_t)min(i0 + u, N - 1) * NP + min(jc0 + jb + 256 * h, NP - 4);
+          Sv[u][h] = *(const v4f*)(a.Sm + o);
+          Lv[u][h] = *(const v4f*)(a.Lm + o);
+        }
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = jb + 256 * h + r;
-        if (j < N) {
-          const float ls = lseS[j], lc = lseC[j];
+        for (int r = 0; r < 4; ++r) {
+          const int jl = jb + 256 * h + r;
+          if (jl < jn) {
+            const float msj = jm[0][jl], zsj = jm[1][jl], mcj = jm[2][jl], zcj = jm[3][jl];
 #pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            c[u] += __expf(Sv[u][h][r] - ls);
-            q[u] = fmaf(__expf(Sv[u][h][r] - lsi[u]), 2.f * Lv[u][h][r] - lc, q[u]);
+            for (int u = 0; u < 2; ++u) {
+              c[u] += __expf(lsub(Sv[u][h][r], msj, zsj));
+              // log P_row + log P_col: G - rl then vanishes where Y is one-hot
+              q[u] = fmaf(__expf(lsub(Sv[u][h][r], ms[u], zs[u])),
+                          lsub(Lv[u][h][r], mr[u], zr[u]) + lsub(Lv[u][h][r], mcj, zcj), q[u]);
+            }
           }
         }
-      }
+    }
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const float cs = wave_sum(c[u]), qs = wave_sum(q[u]);
     const int i = i0 + u;
     if (lane == 0 && i < N) {
-      a.stat[i] = lsi[u];
-      a.stat[(int64_t)N + i] = lri[u];
-      a.stat[2LL * N + i] = lseC[i];
-      a.stat[3LL * N + i] = cs;
-      a.stat[4LL * N + i] = -(qs - lri[u]) * inv2n;
+      float mc, zc;
+      lse_parts(a.part1, 3LL * N, 2LL * N + i, a.Js, mc, zc);
+      const float v[8] = {ms[u], zs[u], mr[u], zr[u], mc, zc, cs, -qs * inv2n};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a.stat[k * (int64_t)N + i] = v[k];
     }
   }
 }
@@ -280,11 +299,8 @@ __global__ void __launch_bounds__(NT) clip_grad_kernel(const ClipK a, float* los
   const int w = threadIdx.x >> 6;
   const int N = a.N;
   const float tau = a.tau, itau = 1.f / tau, inv2n = 0.5f / (float)N;
-  const float* lseS = a.stat;
-  const float* lseR = a.stat + N;
-  const float* lseC = a.stat + 2LL * N;
-  const float* cv = a.stat + 3LL * N;
-  const float* rlv = a.stat + 4LL * N;
+  const float* st = a.stat;   // [8][N]: mS, zS, mR, zR, mC, zC, c, rl
+  const float* rlv = a.stat + 7LL * N;
   if (blockIdx.x == 0 && blockIdx.y == 0) {
     float acc = 0.f;
     for (int k = threadIdx.x; k < N; k += NT) {
@@ -300,14 +316,17 @@ __global__ void __launch_bounds__(NT) clip_grad_kernel(const ClipK a, float* los
   const int i0 = a.g0 + 16 * (int)blockIdx.x;
   const int irow = min(i0 + il, N - 1);
   const int pc = 16 * (int)blockIdx.y;
-  const float lsi = lseS[irow], lri = lseR[irow], lci = lseC[irow], ci = cv[irow], rli = rlv[irow];
+  float si[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) si[k] = st[k * (int64_t)N + irow];
+  const float ci = si[6], rli = si[7];
   const int64_t rowo = (int64_t)irow * a.NP;
   v4f accI = {0.f, 0.f, 0.f, 0.f}, accT = {0.f, 0.f, 0.f, 0.f};
   const int njt = (N + 15) / 16;
   // two j-tiles per step, every load of both issued before any is used
   for (int jt0 = w; jt0 < njt; jt0 += 8) {
     v4f Sv[2], Lv[2], Ltv[2];
-    float sS[2][4], sR[2][4], sC[2][4], scj[2][4], srl[2][4], xi[2][4], xt[2][4];
+    float sj[2][4][8], xi[2][4], xt[2][4];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int jt = min(jt0 + 4 * h, njt - 1);
@@ -318,11 +337,8 @@ __global__ void __launch_bounds__(NT) clip_grad_kernel(const ClipK a, float* los
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = min(jb + r, N - 1);
-        sS[h][r] = lseS[j];
-        sR[h][r] = lseR[j];
-        sC[h][r] = lseC[j];
-        scj[h][r] = cv[j];
-        srl[h][r] = rlv[j];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sj[h][r][k] = st[k * (int64_t)N + j];
         xi[h][r] = a.I[(int64_t)j * a.ldI + pc + il];
         xt[h][r] = a.T[(int64_t)j * a.ldT + pc + il];
       }
@@ -335,11 +351,15 @@ __global__ void __launch_bounds__(NT) clip_grad_kernel(const ClipK a, float* los
         for (int r = 0; r < 4; ++r) {
           const int j = 16 * jt + 4 * g + r;
           const float S = Sv[h][r], Lij = Lv[h][r], Lji = Ltv[h][r];
-          const float Yij = __expf(S - lsi), Yji = __expf(S - sS[h][r]);
-          const float Gij = -(2.f * Lij - lri - sC[h][r]) * inv2n, Gji = -(2.f * Lji - sR[h][r] - lci) * inv2n;
-          const float Dm = (Yij * (Gij - rli) + Yji * (Gji - srl[h][r])) * (0.5f * tau);
-          const float dLij = (__expf(Lij - lri) - 2.f * Yij + __expf(Lij - sC[h][r]) * scj[h][r]) * inv2n;
-          const float dLji = (__expf(Lji - sR[h][r]) - 2.f * Yji + __expf(Lji - lci) * ci) * inv2n;
+          const float* J = sj[h][r];
+          const float Yij = __expf(lsub(S, si[0], si[1])), Yji = __expf(lsub(S, J[0], J[1]));
+          // log-probabilities of L under its row / column softmax, (x - M) - log z
+          const float rij = lsub(Lij, si[2], si[3]), cij = lsub(Lij, J[4], J[5]);
+          const float rji = lsub(Lji, J[2], J[3]), cji = lsub(Lji, si[4], si[5]);
+          const float Gij = -(rij + cij) * inv2n, Gji = -(rji + cji) * inv2n;
+          const float Dm = (Yij * (Gij - rli) + Yji * (Gji - J[7])) * (0.5f * tau);
+          const float dLij = (__expf(rij) - 2.f * Yij + __expf(cij) * J[6]) * inv2n;
+          const float dLji = (__expf(rji) - 2.f * Yji + __expf(cji) * ci) * inv2n;
           const bool ok = j < N;
           const float bD = ok ? Dm : 0.f, bLt = ok ? dLji * itau : 0.f, bL = ok ? dLij * itau : 0.f;
           // dI^T[p][i] += I_j[p] Dm[i][j] + T_j[p] dL[j][i] / tau ; dT^T likewise
@@ -379,7 +399,7 @@ void products_geometry(int64_t N, int& nrep, int& Js) {
   Js = (int)((nb + r - 1) / r);
 }
 
-size_t off_matrices(int64_t N, int Js) { return ((size_t)Js * 3 * N * 2 + 5 * (size_t)N + 3) / 4 * 4; }
+size_t off_matrices(int64_t N, int Js) { return ((size_t)Js * 3 * N * 2 + 8 * (size_t)N + 3) / 4 * 4; }
 
 size_t ws_floats(int64_t N) {
   int nrep, Js;
@@ -413,10 +433,7 @@ int run(const maeclip_clip_args& a, hipStream_t s) {
   const unsigned nb = (unsigned)((N + 15) / 16);
   hipLaunchKernelGGL((clip_products_kernel<NB>), dim3(nb, k.Js), dim3(NT), 0, s, k);
   MC_CHECK_LAUNCH("maeclip_clip_loss(products)");
-  const size_t lds2 = (size_t)2 * k.NP * sizeof(float);
-  if (lds2 > 65536)
-    (void)hipFuncSetAttribute((const void*)clip_stats_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
-  hipLaunchKernelGGL(clip_stats_kernel, dim3((unsigned)((N + 7) / 8)), dim3(NT), lds2, s, k);
+  hipLaunchKernelGGL(clip_stats_kernel, dim3((unsigned)((N + 7) / 8)), dim3(NT), 0, s, k);
   MC_CHECK_LAUNCH("maeclip_clip_loss(stats)");
   const bool g = grad && Ng > 0;
   const int64_t lddI = a.ld_dI ? a.ld_dI : a.P, lddT = a.ld_dT ? a.ld_dT : a.P;

@@ -404,13 +404,13 @@ def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want
     return o, lse
 
 
-def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True):
-    _dev(qkv, o, dout, lse)
+def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=None):
+    _dev(qkv, o, dout, lse, key_mask)
     D = H * hd
     dqkv = torch.empty((B * n, 3 * D), device=qkv.device, dtype=qkv.dtype)
     part = torch.empty((B, 3 * D), device=qkv.device, dtype=torch.float32) if want_colsum else None
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(), dout=dout.data_ptr(), dqkv=dqkv.data_ptr(),
-                   key_mask=None, colsum_partial=_ptr(part), ld_qkv=qkv.stride(0), ld_o=o.stride(0),
+                   key_mask=_ptr(key_mask), colsum_partial=_ptr(part), ld_qkv=qkv.stride(0), ld_o=o.stride(0),
                    ld_dqkv=3 * D, B=B, n=n, H=H, head_dim=hd, dtype=_dt(qkv), scale=scale, dropout_p=0.0, seed=0)
     _call("maeclip_attn_bwd", C.byref(a), _stream())
     return dqkv, part

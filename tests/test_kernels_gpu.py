@@ -121,7 +121,7 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
-@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag"])
+@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag", "rows"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
                                    (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32), (1, 577, 2, 32),
@@ -134,10 +134,15 @@ def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     workgroups per CU; "two3": its 3-workgroups-per-CU register budget at
     hd = 32), dS kept in LDS between the phases ("sds", opt-in), one-pass
     diagonal schedule with dQ accumulated in LDS ("diag": bf16, hd = 32,
-    n <= 256; the default there)."""
+    n <= 256; the default there). fp32 beyond its LDS images (n = 577, the C4
+    decoder) streams 64-row blocks through LDS ("rows"; forced here at every
+    shape, picked by itself at n = 577 in "four")."""
     B, n, H, hd = shape
-    if dtype == torch.float32 and (n > 256 or mode != "four"):
-        pytest.skip("fp32 parity mode: n <= 256, one variant")
+    if dtype == torch.float32 and mode not in ("four", "rows"):
+        pytest.skip("fp32 parity mode: MFMA kernel (two images) or the rows path")
+    if dtype == torch.bfloat16 and mode == "rows":
+        pytest.skip("rows path: fp32 parity mode only")
+    monkeypatch.setenv("MAECLIP_ATTN_ROWS", "1" if mode == "rows" else "0")
     if mode == "diag" and (dtype == torch.float32 or hd != 32 or n > 256):
         pytest.skip("diagonal backward: bf16, hd = 32, n <= 256")
     monkeypatch.setenv("MAECLIP_ATTN_DIAG", "1" if mode == "diag" else "0")
@@ -180,6 +185,27 @@ def test_attention_key_mask(dev):
     o, _ = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
     ref = _attn_ref(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
     assert (o.double() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("rows", [False, True])
+def test_attention_key_mask_f32(dev, rows, monkeypatch):
+    """fp32 parity mode with DistilBERT's key-padding mask, MFMA kernel and the
+    long-sequence rows path; the backward of the rows path honours the mask too."""
+    monkeypatch.setenv("MAECLIP_ATTN_ROWS", "1" if rows else "0")
+    B, n, H, hd = 3, 70, 2, 64
+    qkv = _rand((B * n, 3 * H * hd), torch.float32, dev, seed=14)
+    km = torch.ones((B, n), device=dev)
+    km[1, 10:] = 0
+    km[2, 65:] = 0
+    o, lse = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
+    ref = _attn_ref(qkv, B, n, H, hd, hd ** -0.5, key_mask=km)
+    assert (o.double() - ref).abs().max().item() < 2e-5
+    if rows:
+        dout = _rand((B * n, H * hd), torch.float32, dev, seed=15)
+        dqkv, _ = K.attn_bwd(qkv, o, dout, lse, B, n, H, hd, hd ** -0.5, key_mask=km)
+        x64 = qkv.double().detach().requires_grad_(True)
+        (_attn_ref(x64, B, n, H, hd, hd ** -0.5, key_mask=km) * dout.double()).sum().backward()
+        assert (dqkv.double() - x64.grad).abs().max().item() / x64.grad.abs().max().item() < 1e-4
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -190,8 +190,7 @@ def test_vitl14_336_shapes_bf16_vs_oracle(dev):
     blocks and B = 4 so the fp64 CPU oracle stays fast: bf16 production loss vs
     the oracle on the same weights (rel 2e-2, bf16 operands) and finite grads.
     Patch-embed K = 588 is not a multiple of 64: it takes the GEMM fallback
-    below the v4 kernel. (The fp32 parity mode keeps [n][HD] fp32 images in
-    LDS and is limited to n <= 256 at HD 32.)"""
+    below the v4 kernel. (fp32 at these shapes: test_vitl14_336_parity_fp32_vs_oracle.)"""
     prod, ref = build_pair("bf16", model_name="vit_large_patch14_336", size=336, image_embedding=1024,
                            text_layers=2, mask_ratio=0.75, decoder_embed_dim=512, decoder_depth=2,
                            decoder_num_heads=16, vit_depth=4)
@@ -206,6 +205,37 @@ def test_vitl14_336_shapes_bf16_vs_oracle(dev):
     with torch.no_grad():
         rloss = ref(dict(batch, image=batch["image"].double())).item()
     assert abs(loss.item() - rloss) < 2e-2 * max(1.0, abs(rloss)), (loss.item(), rloss)
+
+
+def test_vitl14_336_parity_fp32_vs_oracle(dev):
+    """C4 shapes in the fp32 parity mode vs the fp64 oracle (BASELINE configs[4]:
+    ViT-L/14 @336, the full 8 x 512-d decoder at n = 577 tokens, hd 32 -- its
+    attention streams 64-row K/V and Q/dO blocks through LDS, the fp32 images
+    of the MFMA kernels do not fit at that n), encoder cut to 4 of 24 blocks
+    and B = 2 so the CPU oracle stays fast. Same bar as C1 / C2: |dloss| <=
+    1e-5 relative, every trainable gradient <= 1e-3 max-rel. The image-branch
+    bias gradients here are sums over the two samples of CLIP-loss rows that
+    nearly cancel (peaked logits ~30): the oracle's own fp32 run is recorded
+    beside the product's deviation as the f32 floor of that case."""
+    import copy
+    prod, ref = build_pair("fp32", model_name="vit_large_patch14_336", size=336, image_embedding=1024,
+                           text_layers=2, mask_ratio=0.75, decoder_embed_dim=512, decoder_depth=8,
+                           decoder_num_heads=16, vit_depth=4)
+    ref32 = copy.deepcopy(ref).float()
+    prod.eval()
+    ref.eval()
+    ref32.eval()
+    batch = make_batch(2, 336, seed=13)
+    loss, rloss = _run(prod, ref, batch, dev)
+    ref32(dict(batch, image=batch["image"].float())).backward()
+    d = abs(loss.item() - rloss.item())
+    worst = _grad_errs(prod, ref)
+    e32 = {name: e for e, name in _grad_errs(ref32, ref)}
+    record_parity("vitl14_336_fp32_vs_oracle", loss_abs=d, loss_rel=d / max(1.0, abs(rloss.item())),
+                  worst_grad_maxrel=worst[0][0], worst_grad=worst[0][1], oracle_fp32_same_grad=e32[worst[0][1]],
+                  oracle_fp32_worst=max(e32.values()))
+    assert d < 1e-3 and d < 1e-5 * max(1.0, abs(rloss.item())), (loss.item(), rloss.item())
+    assert worst[0][0] < 1e-3, [(e, name, e32[name]) for e, name in worst[:5]]
 
 
 def test_vitb_bf16_grads_match_fp32(dev):
