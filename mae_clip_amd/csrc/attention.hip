@@ -699,7 +699,8 @@ attn_bwd_kernel(const maeclip_attn_args a) {
 }
 
 // ======================================================= backward, diagonal
-// bf16, HD = 32, npad <= 256 (the C2/C3 MAE decoder: n = 197): one pass
+// bf16, HD = 32 with npad <= 256 (the C2/C3 MAE decoder: n = 197) and HD = 64
+// with npad <= 224 (the ViT encoders: C1 n = 197, C2 n = 50, C4 n = 145): one pass
 // instead of two. Wave w owns key chunk w (32 keys, K/V fragments in
 // registers) and in round r works query chunk c = (w + r) % NC, so in every
 // round each query chunk is touched by exactly one wave. Per (key chunk, query
@@ -709,13 +710,15 @@ attn_bwd_kernel(const maeclip_attn_args a) {
 // wave that owns the chunk this round; a barrier ends the round). The order
 // in which the waves add to a query chunk is fixed by the schedule, so the
 // result is deterministic, and S / dP / exp are not recomputed for dQ.
-// LDS: Q, dO images, L2 / Dv, dQ f32 [npad][32] (16-B chunks XOR-swizzled by
-// (row >> 1) & 7), NW dS tiles, bias partials: ~78 KB at n = 197 (two
-// workgroups per CU).
-constexpr int DIAG_HD = 32;
-// dQ image: 128-B rows, 16-B chunk ^ (row & 7): conflict-free b128 reads and
-// writes of the (16 rows x 4 chunks) tiles of one MFMA output
-__device__ __forceinline__ int dq_off(int row, int c16) { return row * 128 + ((c16 ^ (row & 7)) << 4); }
+// LDS: Q, dO images, L2 / Dv, dQ f32 [npad][HD] (16-B chunks XOR-swizzled by
+// the row), NW dS tiles, bias partials: ~78 KB at n = 197, HD = 32 (two
+// workgroups per CU); ~142 KB at HD = 64 (one).
+// dQ image: HD f32 per row, 16-B chunk ^ (row & 7) (128-B rows) / (row & 15)
+// (256-B rows): conflict-free b128 reads and writes of the (16 rows x 4
+// chunks) tiles of one MFMA output
+template <int HD> __device__ __forceinline__ int dq_off(int row, int c16) {
+  return row * (4 * HD) + ((c16 ^ (row & (HD / 4 - 1))) << 4);
+}
 // dS tile [32 keys][32 q] bf16, 64-B rows, 8-B unit ^ F(row) with F linear in
 // row bits 1..3 (found by tools/lds_bank_sim.py): conflict-free for both the
 // ds_write_b64 of the MFMA output (row = key, unit = 4u + g) and the
@@ -744,10 +747,11 @@ __device__ __forceinline__ v8s pack8(const v4f& a, const v4f& b) {
   return __builtin_bit_cast(v8s, u);
 }
 
-__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(4)))
+template <int HD>
+__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(HD == 32 ? 4 : 2)))
 attn_bwd_diag_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int HD = DIAG_HD;
+  constexpr int KS = HD / 32, DT = HD / 16, CPR = HD / 8, ROWB = Img<bf16_t, HD>::ROWB, DQB = 4 * HD;
   using I = Img<bf16_t, HD>;
   const int n = a.n, H = a.H;
   const int bid = xcd_chunk_id(blockIdx.x, gridDim.x);
@@ -759,8 +763,8 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   char* Di = smem + img;
   float* L2 = (float*)(smem + 2 * img);
   float* Dv = L2 + npad;
-  char* dQi = (char*)(Dv + npad);                 // f32 [npad][32]
-  char* dst = dQi + npad * 128;                   // NW x [32 keys][32 q] bf16
+  char* dQi = (char*)(Dv + npad);                 // f32 [npad][HD]
+  char* dst = dQi + npad * DQB;                   // NW x [32 keys][32 q] bf16
   float* csv = (float*)(dst + NW * 2048);         // [4 NW][HD] v-bias partials (one row per 16-lane row)
   float* csq = csv + 4 * NW * HD;                 // [4 NW][HD] q-bias partials
   char* myds = dst + wave * 2048;
@@ -779,40 +783,46 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   // B-operand row fragments, K^T as the A operand of dQ^T in the permuted key
   // order of pack8 / dst_frag
   const int kbase = 32 * wave;
-  v8s kf[2], vf[2], kT[2];
+  v8s kf[2][KS], vf[2][KS], kT[DT];
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const int key = min(kbase + 16 * kt + l15, n - 1);
     const bf16_t* kr = qkv + (int64_t)key * a.ld_qkv + HH + h * HD + 8 * g;
-    kf[kt] = *(const v8s*)kr;
-    vf[kt] = *(const v8s*)(kr + HH);
-  }
-  // Q, dO, O chunks: thread -> chunk slots tid and tid + NTH (4 per row)
-  v4u vq[2], vd[2], vo[2];
-  float ls[2];
-  const int cc = threadIdx.x & 3;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = (threadIdx.x + u * NTH) >> 2, rc = min(row, n - 1);
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[kt][ks] = *(const v8s*)(kr + 32 * ks);
+      vf[kt][ks] = *(const v8s*)(kr + HH + 32 * ks);
+    }
+  }
+  // Q, dO, O chunks: thread -> chunk slots tid + u NTH (CPR per row)
+  constexpr int U = CPR / 2;   // npad CPR chunks over NTH = 2 npad threads
+  v4u vq[U], vd[U], vo[U];
+  float ls[U];
+  const int cc = threadIdx.x % CPR;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int row = (threadIdx.x + u * NTH) / CPR, rc = min(row, n - 1);
     vq[u] = *(const v4u*)(qkv + (int64_t)rc * a.ld_qkv + h * HD + 8 * cc);
     vd[u] = *(const v4u*)(dO + (int64_t)rc * a.ld_o + 8 * cc);
     vo[u] = *(const v4u*)(O + (int64_t)rc * a.ld_o + 8 * cc);
     ls[u] = lse[rc];
   }
-  for (int i = threadIdx.x * 4; i < npad * 32; i += 4 * NTH) *(v4f*)(dQi + i * 4) = v4f{0.f, 0.f, 0.f, 0.f};
+  if (HD == 32)   // (HD = 64: the region first holds the K images for K^T, below)
+    for (int i = threadIdx.x * 4; i < npad * HD; i += 4 * NTH) *(v4f*)(dQi + i * 4) = v4f{0.f, 0.f, 0.f, 0.f};
   ASTAMP(6);
   float vs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // v-bias: column sums of dO
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = (threadIdx.x + u * NTH) >> 2;
+  for (int u = 0; u < U; ++u) {
+    const int row = (threadIdx.x + u * NTH) / CPR;
     const bool ok = row < n;
     const v4u z = {0, 0, 0, 0};
     const v4u q = ok ? vq[u] : z, d = ok ? vd[u] : z;
     *(v4u*)(Qi + I::chunk(row, cc)) = q;
     *(v4u*)(Di + I::chunk(row, cc)) = d;
     float dd = chunk_dot<bf16_t>(d, ok ? vo[u] : z);
-    dd += dpp_mov<0xB1>(dd);   // the row's 4 chunks are one lane quad
+    dd += dpp_mov<0xB1>(dd);   // the row's CPR chunks are one lane quad (HD 32) or two
     dd += dpp_mov<0x4E>(dd);
+    if (CPR == 8) dd += dpp_mov<0x141>(dd);   // row_half_mirror: the other quad
     if (cc == 0) {
       Dv[row] = -dd;
       L2[row] = ok ? -ls[u] : -1.0e30f;   // S' = c S: the exponent is S' - lse2
@@ -823,36 +833,47 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
       vs[2 * j + 1] += __uint_as_float(d[j] & 0xffff0000u);
     }
   }
-  // lanes cc, cc + 4, cc + 8, cc + 12 of each 16-lane row: row_shr 4, 8 (DPP)
-  // leave the row's sum for chunk cc in lane 12 + cc
+  // lanes cc, cc + CPR, ... of each 16-lane row: row_shr 4, 8 (DPP) leave the
+  // row's sum for chunk cc in lane 16 - CPR + cc
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    vs[j] += dpp_mov<0x114>(vs[j]);
+    if (CPR == 4) vs[j] += dpp_mov<0x114>(vs[j]);
     vs[j] += dpp_mov<0x118>(vs[j]);
   }
-  // K^T (the A operand of dQ^T) through this wave's dS tile, which is free
-  // until the first round: the wave's 32 K rows as a [32][HD] image (padding
-  // keys zero), read back transposed -- instead of 16 two-byte global loads
-  // per lane
+  // K^T (the A operand of dQ^T) through LDS: the wave's 32 K rows as a
+  // [32][HD] image (padding keys zero), read back transposed -- instead of
+  // 16 DT two-byte global loads per lane. HD 32: this wave's dS tile, free
+  // until the first round; HD 64 (4 KB): the wave's slice of the dQ image,
+  // zeroed afterwards
+  char* kimg = HD == 32 ? myds : dQi + wave * 4096;
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const bool kok = kbase + 16 * kt + l15 < n;
-    *(v8s*)(myds + I::chunk(16 * kt + l15, g)) = kok ? kf[kt] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      *(v8s*)(kimg + I::chunk(16 * kt + l15, 4 * ks + g)) = kok ? kf[kt][ks] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
   }
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) kT[dt] = tr_frag<HD>(myds, 0, 16 * dt, lane);
+  for (int dt = 0; dt < DT; ++dt) kT[dt] = tr_frag<HD>(kimg, 0, 16 * dt, lane);
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const bool kok = kbase + 16 * kt + l15 < n;
-    v8s t;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) t[j] = kok ? (short)f2bf(c * bf2f((bf16_t)kf[kt][j])) : (short)0;
-    kf[kt] = t;
-    vf[kt] = kok ? vf[kt] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ks = 0; ks < KS; ++ks) {
+      v8s t;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = kok ? (short)f2bf(c * bf2f((bf16_t)kf[kt][ks][j])) : (short)0;
+      kf[kt][ks] = t;
+      vf[kt][ks] = kok ? vf[kt][ks] : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  if (HD != 32) {
+    __syncthreads();   // every wave has read its K^T back
+    for (int i = threadIdx.x * 4; i < npad * HD; i += 4 * NTH) *(v4f*)(dQi + i * 4) = v4f{0.f, 0.f, 0.f, 0.f};
   }
   ASTAMP(7);
   __syncthreads();
-  if (a.colsum_partial && (lane & 15) >= 12)
+  if (a.colsum_partial && (lane & 15) >= 16 - CPR)
 #pragma unroll
     for (int j = 0; j < 8; ++j) csv[(4 * wave + (lane >> 4)) * HD + 8 * cc + j] = vs[j];
   ASTAMP(1);
@@ -861,16 +882,18 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   // of 32, so every swizzle below depends on the lane only)
   const int p_ = lane & 3;
   const int qq_ = (lane >> 2) & 3;
-  const int o_rf = I::chunk(l15, g);                     // Q / dO row fragment, + 1024 for u = 1
-  int o_tr[2];                                           // Q / dO transposed, + 1024 for h = 1
+  int o_rf[KS];                                          // Q / dO row fragment, + 16 ROWB for u = 1
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
+  for (int ks = 0; ks < KS; ++ks) o_rf[ks] = I::chunk(l15, 4 * ks + g);
+  int o_tr[DT];                                          // Q / dO transposed, + 16 ROWB for h = 1
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
     const int unit = 4 * dt + p_;
     o_tr[dt] = I::chunk(4 * g + qq_, unit >> 1) + ((unit & 1) << 3);
   }
-  int o_dq[2];                                           // dQ f32, + 2048 for u = 1
+  int o_dq[DT];                                          // dQ f32, + 16 DQB for u = 1
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) o_dq[dt] = dq_off(l15, 4 * dt + g);
+  for (int dt = 0; dt < DT; ++dt) o_dq[dt] = dq_off<HD>(l15, 4 * dt + g);
   int o_sw[2], o_sr[2];                                  // dS tile write (+ 1024 kt = 1) / read (+ 1024 h = 1)
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -878,32 +901,34 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     o_sr[u] = dst_off(4 * g + qq_, 4 * u + p_);
   }
 
-  v4f dv[2][2], dk[2][2];
+  v4f dv[2][DT], dk[2][DT];
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) { dv[kt][dt] = v4f{0, 0, 0, 0}; dk[kt][dt] = v4f{0, 0, 0, 0}; }
+    for (int dt = 0; dt < DT; ++dt) { dv[kt][dt] = v4f{0, 0, 0, 0}; dk[kt][dt] = v4f{0, 0, 0, 0}; }
 
   for (int r = 0; r < NC; ++r) {
     int qc = wave + r;
     qc = qc >= NC ? qc - NC : qc;
     const int q0 = qc * 32;
-    const char* Qr = Qi + q0 * 64;
-    const char* Dr = Di + q0 * 64;
-    v8s qf[2], df[2];
+    const char* Qr = Qi + q0 * ROWB;
+    const char* Dr = Di + q0 * ROWB;
+    v8s qf[2][KS], df[2][KS];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      qf[u] = *(const v8s*)(Qr + o_rf + 1024 * u);
-      df[u] = *(const v8s*)(Dr + o_rf + 1024 * u);
-    }
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        qf[u][ks] = *(const v8s*)(Qr + o_rf[ks] + 16 * ROWB * u);
+        df[u][ks] = *(const v8s*)(Dr + o_rf[ks] + 16 * ROWB * u);
+      }
     // transposed Q / dO fragments (A operands of dK^T / dV^T): rows q0..q0+31
-    v8s qT[2], dT[2];
+    v8s qT[DT], dT[DT];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
+    for (int dt = 0; dt < DT; ++dt) {
       v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Qr + o_tr[dt]));
-      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Qr + o_tr[dt] + 1024));
+      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Qr + o_tr[dt] + 16 * ROWB));
       v4s y0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Dr + o_tr[dt]));
-      v4s y1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Dr + o_tr[dt] + 1024));
+      v4s y1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, Dr + o_tr[dt] + 16 * ROWB));
       qT[dt] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
       dT[dt] = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
     }
@@ -920,8 +945,12 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
       for (int u = 0; u < 2; ++u) {
         // S' - lse2 [q = 4g+i][key = lane&15] and dP - Dv, row constants as the
         // initial accumulators
-        const v4f s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[u], kf[kt], l2[u], 0, 0, 0);
-        const v4f dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[u], vf[kt], dvr[u], 0, 0, 0);
+        v4f s = l2[u], dp = dvr[u];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[u][ks], kf[kt][ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[u][ks], vf[kt][ks], dp, 0, 0, 0);
+        }
         // P clamped to [0, 1] by the exp's output modifier (free): softmax
         // probabilities never exceed 1, and a padding key (zero K row: S' = 0,
         // P = 2^-lse2) can then never overflow into 0 * inf = NaN in dQ
@@ -935,21 +964,21 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
       }
       const v8s pp = pack8(P[0], P[1]), ps = pack8(dS[0], dS[1]);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         dv[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dT[dt], pp, dv[kt][dt], 0, 0, 0);
         dk[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT[dt], ps, dk[kt][dt], 0, 0, 0);
       }
     }
     // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] for this wave's 32 keys
-    char* dQr = dQi + q0 * 128;
+    char* dQr = dQi + q0 * DQB;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, myds + o_sr[u]));
       v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, myds + o_sr[u] + 1024));
       const v8s bds = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        v4f* pq = (v4f*)(dQr + o_dq[dt] + 2048 * u);
+      for (int dt = 0; dt < DT; ++dt) {
+        v4f* pq = (v4f*)(dQr + o_dq[dt] + 16 * DQB * u);
         *pq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kT[dt], bds, *pq, 0, 0, 0);
       }
     }
@@ -964,7 +993,7 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     if (key < n) {
       bf16_t* rowp = dqkv + (int64_t)key * a.ld_dqkv + h * HD;
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         st4<bf16_t>(rowp + HH + 16 * dt + 4 * g, dk[kt][dt] * a.scale);
         st4<bf16_t>(rowp + 2 * HH + 16 * dt + 4 * g, dv[kt][dt]);
       }
@@ -973,9 +1002,10 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   ASTAMP(3);
   // dQ rows: thread -> (row, 4 columns); q-bias partial per (row group, column)
   float cq[4] = {0.f, 0.f, 0.f, 0.f};
-  const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3, nrg = NTH >> 3;
+  constexpr int C4N = HD / 4;   // 16-B chunks per dQ row
+  const int c4 = threadIdx.x % C4N, rg = threadIdx.x / C4N, nrg = NTH / C4N;
   for (int row = rg; row < n; row += nrg) {
-    const v4f v = *(const v4f*)(dQi + dq_off(row, c4)) * a.scale;
+    const v4f v = *(const v4f*)(dQi + dq_off<HD>(row, c4)) * a.scale;
     st4<bf16_t>(dqkv + (int64_t)row * a.ld_dqkv + h * HD + 4 * c4, v);
 #pragma unroll
     for (int i = 0; i < 4; ++i) cq[i] += v[i];
@@ -984,10 +1014,12 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   if (a.colsum_partial) {
     // reduce the row groups of a wave (lanes with equal c4) by shuffles, then
     // one partial row per wave in cs
-    // lanes c4 and c4 + 8 of each 16-lane row (row_shr 8): the row's sum in lane 8 + c4
+    // HD 32: lanes c4 and c4 + 8 of each 16-lane row (row_shr 8): the row's
+    // sum in lane 8 + c4; HD 64: a 16-lane row is one dQ row already
+    if (HD == 32)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cq[i] += dpp_mov<0x118>(cq[i]);
-    if ((lane & 15) >= 8)
+      for (int i = 0; i < 4; ++i) cq[i] += dpp_mov<0x118>(cq[i]);
+    if ((lane & 15) >= (HD == 32 ? 8 : 0))
 #pragma unroll
       for (int i = 0; i < 4; ++i) csq[(4 * wave + (lane >> 4)) * HD + 4 * c4 + i] = cq[i];
     __syncthreads();
@@ -1212,10 +1244,10 @@ int run_rows(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   return 0;
 }
 
-size_t bwd_diag_lds(int n) {
+template <int HD> size_t bwd_diag_lds(int n) {
   const int npad = (n + 31) & ~31, nw = npad / 32;
-  return (size_t)2 * npad * Img<bf16_t, DIAG_HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 128 +
-         (size_t)nw * 2048 + (size_t)8 * nw * DIAG_HD * 4;
+  return (size_t)2 * npad * Img<bf16_t, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 4 * HD +
+         (size_t)nw * 2048 + (size_t)8 * nw * HD * 4;
 }
 
 template <typename T, int HD> size_t fwd_lds(int n) {
@@ -1295,15 +1327,22 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   MC_CHECK_ARG(!bwd || !a.key_mask, "maeclip_attn_bwd: key_mask is supported by the fp32 rows path only");
   dim3 grid((unsigned)(a.B * a.H));
-  if constexpr (std::is_same<T, bf16_t>::value && HD == DIAG_HD) {
-    // one-pass diagonal backward (MAECLIP_ATTN_DIAG=0 turns it off)
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    // one-pass diagonal backward: the default at HD 32 up to npad 256
+    // (MAECLIP_ATTN_DIAG=0 turns it off); opt-in (MAECLIP_ATTN_DIAG=1) at HD 64
+    // while its LDS fits (npad <= 224). Measured slower there (C1 encoder 323
+    // vs 280 us, C4 encoder 157 vs 123, C2 encoder 49 vs 46;
+    // profiles/r03/attn_diag64_ab.txt): the 56 KB f32 dQ image leaves one
+    // workgroup per CU, whose ~140 KB prologue then has nothing to overlap with.
     const char* e = getenv("MAECLIP_ATTN_DIAG");
     const int npad = (a.n + 31) & ~31;
-    if (bwd && npad <= 256 && !(e && *e == '0')) {
-      const size_t ld = bwd_diag_lds(a.n);
+    const size_t ld = bwd_diag_lds<HD>(a.n);
+    const bool want = HD == 32 ? !(e && *e == '0') : (e && *e == '1');
+    if (bwd && npad <= 256 && ld <= 163840 && want && !a.key_mask) {
       if (ld > 65536)
-        (void)hipFuncSetAttribute((const void*)attn_bwd_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ld);
-      hipLaunchKernelGGL(attn_bwd_diag_kernel, grid, dim3(2 * npad), ld, s, a);
+        (void)hipFuncSetAttribute((const void*)attn_bwd_diag_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)ld);
+      hipLaunchKernelGGL(attn_bwd_diag_kernel<HD>, grid, dim3(2 * npad), ld, s, a);
       MC_CHECK_LAUNCH("maeclip_attn_bwd(diag)");
       return 0;
     }

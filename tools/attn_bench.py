@@ -11,7 +11,8 @@ import torch.nn.functional as F
 from mae_clip_amd import kernels as K
 
 dev = torch.device("cuda")
-SHAPES = [("enc", 256, 50, 12, 64), ("dec", 256, 197, 16, 32), ("text", 256, 25, 12, 64)]
+SHAPES = [("enc", 256, 50, 12, 64), ("dec", 256, 197, 16, 32), ("text", 256, 25, 12, 64),
+          ("C1 enc", 256, 197, 12, 64), ("C4 enc", 128, 145, 16, 64), ("C4 dec", 128, 577, 16, 32)]
 
 
 def time_fn(fn, reps=20):
