@@ -228,25 +228,39 @@ __global__ void __launch_bounds__(NT) clip_stats_kernel(const ClipK a) {
   const int N = a.N, NP = a.NP;
   const float inv2n = 0.5f / (float)N;
   const int i0 = 8 * (int)blockIdx.x + 2 * w;
-  float ms[2], zs[2], mr[2], zr[2];
+  // row statistics of L (L rows); those of S rows and L^T rows are column
+  // statistics (S symmetric, L^T rows = L columns): read from the first staged
+  // chunk, or combined here for rows past it
+  float ms[2], zs[2], mr[2], zr[2], mc[2], zc[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = min(i0 + u, N - 1);
-    lse_parts(a.part1, 3LL * N, i, a.Js, ms[u], zs[u]);
-    lse_parts(a.part1, 3LL * N, (int64_t)N + i, a.Js, mr[u], zr[u]);
-  }
+  for (int u = 0; u < 2; ++u) lse_parts(a.part1, 3LL * N, (int64_t)N + min(i0 + u, N - 1), a.Js, mr[u], zr[u]);
   float c[2] = {0.f, 0.f}, q[2] = {0.f, 0.f};
   for (int jc0 = 0; jc0 < N; jc0 += JC) {
     const int jn = min(JC, N - jc0);
     __syncthreads();   // the previous chunk's reads are done
-    for (int t = threadIdx.x; t < 2 * JC; t += NT) {
-      const int j = t % JC, which = t / JC;
-      float M = 0.f, lz = 0.f;
-      if (j < jn) lse_parts(a.part1, 3LL * N, (which ? 2LL * N : 0LL) + jc0 + j, a.Js, M, lz);
+    for (int t = threadIdx.x; t < 2 * jn; t += NT) {
+      const int j = t % jn, which = t / jn;
+      float M, lz;
+      lse_parts(a.part1, 3LL * N, (which ? 2LL * N : 0LL) + jc0 + j, a.Js, M, lz);
       jm[2 * which][j] = M;
       jm[2 * which + 1][j] = lz;
     }
     __syncthreads();
+    if (jc0 == 0) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = min(i0 + u, N - 1);
+        if (i < jn) {
+          ms[u] = jm[0][i];
+          zs[u] = jm[1][i];
+          mc[u] = jm[2][i];
+          zc[u] = jm[3][i];
+        } else {
+          lse_parts(a.part1, 3LL * N, i, a.Js, ms[u], zs[u]);
+          lse_parts(a.part1, 3LL * N, 2LL * N + i, a.Js, mc[u], zc[u]);
+        }
+      }
+    }
     for (int jb = 4 * lane; jb < jn; jb += 512) {
       v4f Sv[2][2], Lv[2][2];
 #pragma unroll
@@ -280,9 +294,7 @@ __global__ void __launch_bounds__(NT) clip_stats_kernel(const ClipK a) {
     const float cs = wave_sum(c[u]), qs = wave_sum(q[u]);
     const int i = i0 + u;
     if (lane == 0 && i < N) {
-      float mc, zc;
-      lse_parts(a.part1, 3LL * N, 2LL * N + i, a.Js, mc, zc);
-      const float v[8] = {ms[u], zs[u], mr[u], zr[u], mc, zc, cs, -qs * inv2n};
+      const float v[8] = {ms[u], zs[u], mr[u], zr[u], mc[u], zc[u], cs, -qs * inv2n};
 #pragma unroll
       for (int k = 0; k < 8; ++k) a.stat[k * (int64_t)N + i] = v[k];
     }

@@ -23,6 +23,9 @@ for s in $STEPS; do
     benchq)
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-parity --steps 20 > gpurun_out/benchq_${TAG}.json 2> gpurun_out/benchq_${TAG}.err || { tail -30 gpurun_out/benchq_${TAG}.err; exit 1; }
       cat gpurun_out/benchq_${TAG}.json ;;
+    benchdp)   # the data-parallel code path at world 1 (RCCL group, gathers, bucketed all-reduce)
+      timeout -k 10 300 python -u bench.py --dp --no-cpu-baseline --no-parity --steps 20 > gpurun_out/benchdp_${TAG}.json 2> gpurun_out/benchdp_${TAG}.err || { tail -30 gpurun_out/benchdp_${TAG}.err; exit 1; }
+      cat gpurun_out/benchdp_${TAG}.json ;;
     gemmcal)
       timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/gemmcal_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/gemmcal_${TAG}.jsonl; exit 1; }
       cat gpurun_out/gemmcal_${TAG}.jsonl ;;

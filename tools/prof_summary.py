@@ -6,7 +6,7 @@ rows = list(csv.DictReader(open(path)))
 groups = {}
 for r in rows:
     n = r['Name']
-    g = ('gemm' if 'gemm' in n else 'attn' if 'attn_' in n else 'ln' if 'ln_' in n else
+    g = ('gemm wgrad' if 'wgrad' in n else 'gemm' if 'gemm' in n else 'attn' if 'attn_' in n else 'ln' if 'ln_' in n else
          'adamw/cast' if ('adamw' in n or 'cast_multi' in n) else 'colsum' if 'colsum' in n or 'vec_sum' in n else
          'torch' if 'at::native' in n or 'rocclr' in n else 'mae/other')
     groups[g] = groups.get(g, 0.0) + float(r['TotalDurationNs'])
