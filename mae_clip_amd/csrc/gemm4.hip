@@ -48,8 +48,7 @@ __device__ uint64_t g_stamps[256 * 8 * 2 * 4];
 #endif
 
 constexpr int HALF = 16384;          // bytes per half image (128 rows/cols x 64 k x bf16)
-constexpr int BUF = 4 * HALF;        // one K-tile
-constexpr int LDS_BYTES = 2 * BUF;   // 128 KiB
+constexpr int BUF = 4 * HALF;        // one K-tile (two stages: 128 KiB)
 // BM = 192 (plain launches, KC A operand): 96-row A halves (12 KiB), waves own
 // 96 x 64 output blocks (3 x 4 fragments per quadrant row), 6 row fragments;
 // chosen when it needs fewer full-tile rounds of the grid (encoder N = 768
@@ -268,6 +267,21 @@ __device__ __forceinline__ void epilogue4_tile(float* __restrict__ t, v4f (&acc)
 // sa / sb (fp8 only): per-row dequantisation scale of A [M] and per-column
 // scale of B [N]; the product scales the accumulator before alpha / bias.
 constexpr int EPI_SCR = 4096;   // bytes of epilogue scratch per wave
+// epilogue streams (aux / residual reads, C / aux_out writes) touch each byte
+// once: non-temporal, so they do not evict the A / B panels the XCD's tiles share
+#ifndef GEMM4_EPI_NT
+#define GEMM4_EPI_NT 3   // 1: loads, 2: stores
+#endif
+#if GEMM4_EPI_NT & 1
+#define NT_LD(p) __builtin_nontemporal_load(p)
+#else
+#define NT_LD(p) (*(p))
+#endif
+#if GEMM4_EPI_NT & 2
+#define NT_ST(v, p) __builtin_nontemporal_store(v, p)
+#else
+#define NT_ST(v, p) (*(p) = (v))
+#endif
 __device__ __forceinline__ int scr_off(int r, int u) { return r * 256 + ((u ^ r) << 4); }
 
 template <typename OutT, int EPI, bool F8 = false, int BM = 256>
@@ -314,11 +328,11 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int m = min(rbase + 16 * c + RPI * q, M - 1);
-      if (LOAD_AUX) ax[buf][q] = *(const auxv_t*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + nc);
+      if (LOAD_AUX) ax[buf][q] = NT_LD((const auxv_t*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + nc));
       if (LOAD_RES && has_res) {
         const float* rp = args.resid + off + (int64_t)m * args.ldr + nc;
 #pragma unroll
-        for (int v = 0; v < VPL / 4; ++v) rs[buf][q][v] = *(const v4f*)(rp + 4 * v);
+        for (int v = 0; v < VPL / 4; ++v) rs[buf][q][v] = NT_LD((const v4f*)(rp + 4 * v));
       }
     }
   };
@@ -370,10 +384,10 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
           if (L8) {
             const v4u pk = {pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4 % VPL], d[5 % VPL]),
                             pack2bf(d[6 % VPL], d[7 % VPL])};
-            *(v4u*)ap = pk;
+            NT_ST(pk, (v4u*)ap);
           } else {
             const v2u pk = {pack2bf(d[0], d[1]), pack2bf(d[2], d[3])};
-            *(v2u*)ap = pk;
+            NT_ST(pk, (v2u*)ap);
           }
         }
       }
@@ -410,9 +424,9 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
         if (L8) {
           const v4u pk = {pack2bf(x[0], x[1]), pack2bf(x[2], x[3]), pack2bf(x[4 % VPL], x[5 % VPL]),
                           pack2bf(x[6 % VPL], x[7 % VPL])};
-          *(v4u*)cp = pk;
+          NT_ST(pk, (v4u*)cp);
         } else {
-          *(v4f*)cp = v4f{x[0], x[1], x[2], x[3]};
+          NT_ST((v4f{x[0], x[1], x[2], x[3]}), (v4f*)cp);
         }
       }
     }
