@@ -48,7 +48,6 @@ __device__ uint64_t g_stamps[256 * 8 * 2 * 4];
 #endif
 
 constexpr int HALF = 16384;          // bytes per half image (128 rows/cols x 64 k x bf16)
-constexpr int BUF = 4 * HALF;        // one K-tile (two stages: 128 KiB)
 // BM = 192 (plain launches, KC A operand): 96-row A halves (12 KiB), waves own
 // 96 x 64 output blocks (3 x 4 fragments per quadrant row), 6 row fragments;
 // chosen when it needs fewer full-tile rounds of the grid (encoder N = 768
