@@ -276,13 +276,42 @@ __global__ void __launch_bounds__(NTH) adamw_multi_kernel(const maeclip_mt_entry
     step_size = hp.lr / (1.f - powf(b1, t));
     bc2_sqrt = sqrtf(1.f - powf(b2, t));
   }
+  auto upd = [&](float g, float& pi, float& mi, float& vi) {
+    g *= hp.grad_scale;
+    pi *= decay;
+    mi = b1 * mi + (1.f - b1) * g;
+    vi = b2 * vi + (1.f - b2) * g * g;
+    pi -= step_size * mi / (sqrtf(vi) / bc2_sqrt + hp.eps);
+  };
+  // 16-B vectors when the entry allows (every tensor of the path does); the
+  // fp32 streams are non-temporal -- read and written once per step, they would
+  // otherwise evict the next forward's operands -- the bf16 shadow is not
+  const bool vec = (n & 3) == 0 && ((((uintptr_t)p) | ((uintptr_t)gr) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (!sh || (((uintptr_t)sh) & 7) == 0);
+  if (vec) {
+    for (int64_t i = base + 4 * threadIdx.x; i < base + CHUNK && i < n; i += 4 * NTH) {
+      const v4f g = __builtin_nontemporal_load((const v4f*)(gr + i));
+      v4f pv = __builtin_nontemporal_load((const v4f*)(p + i));
+      v4f mv = __builtin_nontemporal_load((const v4f*)(m + i));
+      v4f vv = __builtin_nontemporal_load((const v4f*)(v + i));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = pv[j], mj = mv[j], vj = vv[j];
+        upd(g[j], pj, mj, vj);
+        pv[j] = pj;
+        mv[j] = mj;
+        vv[j] = vj;
+      }
+      __builtin_nontemporal_store(pv, (v4f*)(p + i));
+      __builtin_nontemporal_store(mv, (v4f*)(m + i));
+      __builtin_nontemporal_store(vv, (v4f*)(v + i));
+      if (sh) *(v2u*)(sh + i) = v2u{pack2bf(pv[0], pv[1]), pack2bf(pv[2], pv[3])};
+    }
+    return;
+  }
   for (int64_t i = base + threadIdx.x; i < base + CHUNK && i < n; i += NTH) {
-    const float g = gr[i] * hp.grad_scale;
-    float pi = p[i] * decay;
-    const float mi = b1 * m[i] + (1.f - b1) * g;
-    const float vi = b2 * v[i] + (1.f - b2) * g * g;
-    const float denom = sqrtf(vi) / bc2_sqrt + hp.eps;
-    pi -= step_size * mi / denom;
+    float pi = p[i], mi = m[i], vi = v[i];
+    upd(gr[i], pi, mi, vi);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;

@@ -24,13 +24,27 @@ namespace {
 constexpr int NTH = 256;
 constexpr int MAXC = 8;  // chunks of 4 elements per lane -> D <= 2048
 
-template <int NC, typename T>
+// non-temporal streams (LN_NT bits): 1 the forward's saved residual-stream
+// copy (xsum, read again only by the backward), 2 the backward's read of it,
+// 4 the backward's f32 dx
+#ifndef LN_NT
+#define LN_NT 7
+#endif
+template <typename T> __device__ __forceinline__ v4f ld4_nt(const T* p);
+template <> __device__ __forceinline__ v4f ld4_nt<float>(const float* p) { return __builtin_nontemporal_load((const v4f*)p); }
+template <> __device__ __forceinline__ v4f ld4_nt<bf16_t>(const bf16_t* p) {
+  const v2u u = __builtin_nontemporal_load((const v2u*)p);
+  return v4f{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+             __uint_as_float(u[1] & 0xffff0000u)};
+}
+
+template <int NC, typename T, bool NT = false>
 __device__ __forceinline__ void load_row(float (&v)[NC][4], const T* p, int D, int lane) {
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int e = c * 256 + lane * 4;
     if (e < D) {
-      v4f t = ld4<T>(p + e);
+      v4f t = NT ? ld4_nt<T>(p + e) : ld4<T>(p + e);
       v[c][0] = t[0]; v[c][1] = t[1]; v[c][2] = t[2]; v[c][3] = t[3];
     } else {
       v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
@@ -117,7 +131,11 @@ __global__ void __launch_bounds__(NTH) ln_fwd_kernel(const maeclip_ln_fwd_args a
   for (int c = 0; c < NC; ++c) {
     const int e = c * 256 + lane * 4;
     if (e >= D) continue;
-    if (a.xsum_out) *(v4f*)(a.xsum_out + row * a.ldxs + e) = v4f{v[c][0], v[c][1], v[c][2], v[c][3]};
+    if (a.xsum_out) {
+      const v4f t = {v[c][0], v[c][1], v[c][2], v[c][3]};
+      if (LN_NT & 1) __builtin_nontemporal_store(t, (v4f*)(a.xsum_out + row * a.ldxs + e));
+      else *(v4f*)(a.xsum_out + row * a.ldxs + e) = t;
+    }
     const v4f gm = *(const v4f*)(a.gamma + e);
     const v4f bt = *(const v4f*)(a.beta + e);
     v4f y;
@@ -152,7 +170,7 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
     // every load of the row issued together (one HBM round trip per row)
     float dy[NC][4], x[NC][4], dr[NC][4];
     load_row<NC, GT>(dy, (const GT*)a.dy + row * a.lddy, D, lane);
-    load_row<NC, XT>(x, (const XT*)a.x + row * a.ldx, D, lane);
+    load_row<NC, XT, (LN_NT & 2) != 0>(x, (const XT*)a.x + row * a.ldx, D, lane);
     if (a.dres) load_row<NC, float>(dr, a.dres + row * a.lddx, D, lane);
     const bool pool = a.dres_pool != nullptr;
     if (pool) {   // global_pool="avg" backward: 1/(n-1) of the pooled gradient, 0 for the cls row
@@ -195,7 +213,8 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
         dy[c][j] = as_stored<bf16_t>(d);
         amax = fmaxf(amax, fabsf(dy[c][j]));
       }
-      *(v4f*)(a.dx + row * a.lddx + e) = o;
+      if (LN_NT & 4) __builtin_nontemporal_store(o, (v4f*)(a.dx + row * a.lddx + e));
+      else *(v4f*)(a.dx + row * a.lddx + e) = o;
       if (a.dx_bf) st4<bf16_t>((bf16_t*)a.dx_bf + row * a.lddx_bf + e, o);
     }
     if (a.q8) quant_row_fp8<NC>(dy, amax, a.q8_fmt == MAECLIP_FP8_E5M2, (uint8_t*)a.q8 + row * a.ldq8, a.q8_scale + row, D, lane);
