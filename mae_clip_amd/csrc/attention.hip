@@ -39,6 +39,16 @@ bool getenv_flag(const char* name) {
   const char* v = getenv(name);
   return v && *v && *v != '0';
 }
+// Q / K / V / O / dO are read once per (sample, head): non-temporal loads, so
+// they do not evict what the next kernels reuse (ATTN_NT=0 turns it off)
+#ifndef ATTN_NT
+#define ATTN_NT 1
+#endif
+#if ATTN_NT
+#define ANT(p) __builtin_nontemporal_load(p)
+#else
+#define ANT(p) (*(p))
+#endif
 #define NW ((int)(blockDim.x >> 6))
 #define NTH ((int)blockDim.x)
 constexpr float LOG2E = 1.4426950408889634f;
@@ -82,7 +92,7 @@ __device__ __forceinline__ void load_imgs(char* const (&lds)[NI], const T* const
       const bool ok = id < total && row < n;
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        v[u][i] = ok ? *(const v4u*)(g[i] + (int64_t)row * ld + c * (16 / sizeof(T))) : v4u{0, 0, 0, 0};
+        v[u][i] = ok ? ANT((const v4u*)(g[i] + (int64_t)row * ld + c * (16 / sizeof(T)))) : v4u{0, 0, 0, 0};
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -136,13 +146,13 @@ __device__ __forceinline__ void bwd_prologue(char* Qi, char* Ki, char* Vi, char*
       const bool ok = id < total && row < n;
       const int64_t oq = (int64_t)row * ld_qkv + c * EPC, oo = (int64_t)row * ld_o + c * EPC;
       const v4u z = {0, 0, 0, 0};
-      vq[u] = ok ? *(const v4u*)(q + oq) : z;
+      vq[u] = ok ? ANT((const v4u*)(q + oq)) : z;
       if (KV) {
-        vk[u] = ok ? *(const v4u*)(k + oq) : z;
-        vv[u] = ok ? *(const v4u*)(v + oq) : z;
+        vk[u] = ok ? ANT((const v4u*)(k + oq)) : z;
+        vv[u] = ok ? ANT((const v4u*)(v + oq)) : z;
       }
-      vd[u] = ok ? *(const v4u*)(dO + oo) : z;
-      vo[u] = ok ? *(const v4u*)(O + oo) : z;
+      vd[u] = ok ? ANT((const v4u*)(dO + oo)) : z;
+      vo[u] = ok ? ANT((const v4u*)(O + oo)) : z;
       ls[u] = (ok && c == 0) ? -lse[row] * inv_c : -1.0e30f;
     }
 #pragma unroll
@@ -176,7 +186,7 @@ template <int HD> struct RowFrag<bf16_t, HD> {
     v = *(const v8s*)(img + Img<bf16_t, HD>::chunk(row, 4 * ks + (lane >> 4)));
   }
   __device__ __forceinline__ void glob(const bf16_t* p, int ks, int lane, bool ok) {
-    v = ok ? *(const v8s*)(p + 32 * ks + 8 * (lane >> 4)) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+    v = ok ? ANT((const v8s*)(p + 32 * ks + 8 * (lane >> 4))) : v8s{0, 0, 0, 0, 0, 0, 0, 0};
   }
 };
 template <int HD> struct RowFrag<float, HD> {
@@ -790,8 +800,8 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     const bf16_t* kr = qkv + (int64_t)key * a.ld_qkv + HH + h * HD + 8 * g;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      kf[kt][ks] = *(const v8s*)(kr + 32 * ks);
-      vf[kt][ks] = *(const v8s*)(kr + HH + 32 * ks);
+      kf[kt][ks] = ANT((const v8s*)(kr + 32 * ks));
+      vf[kt][ks] = ANT((const v8s*)(kr + HH + 32 * ks));
     }
   }
   // Q, dO, O chunks: thread -> chunk slots tid + u NTH (CPR per row)
@@ -802,9 +812,9 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int row = (threadIdx.x + u * NTH) / CPR, rc = min(row, n - 1);
-    vq[u] = *(const v4u*)(qkv + (int64_t)rc * a.ld_qkv + h * HD + 8 * cc);
-    vd[u] = *(const v4u*)(dO + (int64_t)rc * a.ld_o + 8 * cc);
-    vo[u] = *(const v4u*)(O + (int64_t)rc * a.ld_o + 8 * cc);
+    vq[u] = ANT((const v4u*)(qkv + (int64_t)rc * a.ld_qkv + h * HD + 8 * cc));
+    vd[u] = ANT((const v4u*)(dO + (int64_t)rc * a.ld_o + 8 * cc));
+    vo[u] = ANT((const v4u*)(O + (int64_t)rc * a.ld_o + 8 * cc));
     ls[u] = lse[rc];
   }
   if (HD == 32)   // (HD = 64: the region first holds the K images for K^T, below)
