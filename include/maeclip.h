@@ -469,9 +469,12 @@ int32_t maeclip_mae_loss_bwd_partial_rows(int32_t B, int32_t L);
 
 /* ------------------------------------------------------------- CLIP loss
  * CLIPModel.forward loss (CLIP.py:34-43) + cross_entropy (CLIP.py:46-52), fp32,
- * fused and deterministic: the all-pairs products once on the exact-f32 MFMA
- * (S, L, L^T kept in the workspace), then ONE launch for statistics, loss and
- * gradient rows at N <= 512, three (statistics, gradient, reduction) above.
+ * fused and deterministic, three launches at every N: the all-pairs products
+ * once on the exact-f32 MFMA (S, L, L^T kept in the workspace, online row-LSE
+ * partials), one statistics pass over the stored rows (row / column LSE, the
+ * column sums of the soft targets, per-row losses and the loss), and the
+ * gradient rows of the requested slice (no reduction launch). Above N = 2048
+ * the statistics pass stages the column statistics per 2048-column chunk.
  * Any N >= 1; P in {64, 128, 256, 512}. I, T: [N, P] (row strides ld_I/ld_T, 0 = P, 16-B aligned rows).
  * loss: device scalar. row_loss_out (optional, [N]): rl_i with loss = sum rl_i.
  * dI, dT optional: d loss / d I, T for the rows [grad_row0, grad_row0 +

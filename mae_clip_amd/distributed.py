@@ -41,24 +41,38 @@ def all_gather_rows(x, group=None):
     return out
 
 
+_CTRL = {}
+
+
+def control_group(group=None):
+    """A gloo group over the same ranks as `group`, for host-side control
+    messages (batch-size checks): a collective on it moves CPU memory only, so
+    it never synchronises the host with the GPU stream. Created collectively
+    by DataParallel.__init__ (every rank constructs one); None for a group
+    that is already gloo."""
+    key = group if group is not None else dist.group.WORLD
+    if dist.get_backend(group) == "gloo":
+        return None
+    if key not in _CTRL:
+        _CTRL[key] = dist.new_group(ranks=dist.get_process_group_ranks(key), backend="gloo")
+    return _CTRL[key]
+
+
 def check_equal_rows(n, group=None, device=None):
     """Raise if the ranks hold different local batch sizes.
 
     all_gather_into_tensor and the gradient row slice (rank * B, B) of the
     sharded CLIP loss both assume every rank has the same B; a ragged last
     batch (the reference's DataLoader keeps it, main.py:42-47) would otherwise
-    hang or fail inside RCCL. One tiny MAX all-reduce of (B, -B) per eager
-    step; skipped under graph capture (a captured step has fixed shapes on
-    every rank by construction)."""
+    hang or fail inside RCCL. One MAX all-reduce of (B, -B) per eager step, on
+    the host over the gloo control group (no device sync: the host keeps
+    running ahead of the GPU); skipped under graph capture (a captured step has
+    fixed shapes on every rank by construction)."""
     if device is not None and device.type == "cuda" and torch.cuda.is_current_stream_capturing():
         return
-    t = torch.tensor([n, -n], dtype=torch.int64, device=device)
-    if _staged(group, t):
-        h = t.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
-        t = h
-    else:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    t = torch.tensor([n, -n], dtype=torch.int64)
+    ctrl = control_group(group)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl if ctrl is not None else group)
     hi, lo = int(t[0]), -int(t[1])
     if hi != lo:
         raise RuntimeError(f"data parallel: ranks hold different local batch sizes ({lo}..{hi}); "
@@ -104,7 +118,9 @@ class GradArena:
         off = 0
         for p in self.params:
             self.offsets[id(p)] = (off, p.numel(), tuple(p.shape))
-            off += p.numel()
+            # slots start on 16-B boundaries (the flat cast / reduction kernels
+            # take vector accesses); the padding stays zero and sums to zero
+            off += (p.numel() + 3) // 4 * 4
         self.flat = torch.zeros(off, device=device, dtype=torch.float32)
 
         # parameters whose slot has been handed out since the last forward
@@ -161,6 +177,7 @@ class DataParallel:
         self.grad_dtype = grad_dtype
         self.world = dist.get_world_size(group)
         model.process_group = group if group is not None else dist.group.WORLD
+        control_group(group)   # collective: every rank creates the host control group here
         self.params = [p for p in model.parameters() if p.requires_grad]
         if broadcast:
             with torch.no_grad():

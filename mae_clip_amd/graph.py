@@ -49,6 +49,25 @@ class CapturedStep:
         self.captures = 0
         self.hp_key = None
         self.graph_grads = None
+        self.state_key = None
+
+    def _state_key(self):
+        """What a replay bakes in besides the batch: every parameter's storage
+        and version (load_state_dict, in-place edits, another optimizer bump
+        p._version) and the optimizer state buffers (optimizer.load_state_dict
+        replaces them). The captured forward reads bf16 weight shadows that only
+        the fused AdamW keeps current, and the frozen text tower's cached bf16
+        weights, so a change here means the graph would replay stale weights.
+        Writes through p.data are invisible to _version: call invalidate()."""
+        params = tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+        st = tuple(t.data_ptr() for s in self.opt.state.values() for t in s.values() if torch.is_tensor(t))
+        return params, st
+
+    def invalidate(self):
+        """Drop the captured graph: the next step runs eagerly (re-casting the
+        weight shadows from the fp32 masters) and the one after re-captures."""
+        self.graph = None
+        self.calls = 0
 
     def _hparams(self):
         """Optimizer hyper-parameters baked into the captured AdamW launch."""
@@ -90,6 +109,7 @@ class CapturedStep:
         self.graph, self.loss = g, loss.detach()
         self.hp_key = self._hparams()
         self.graph_grads = [(p, p.grad) for grp in self.opt.param_groups for p in grp["params"]]
+        self.state_key = self._state_key()
         self.captures += 1
 
     def _fits(self, batch):
@@ -103,6 +123,8 @@ class CapturedStep:
         partial batch of an epoch: the reference's DataLoader keeps it,
         main.py:42-47) runs as an eager step; a change of lr / betas / eps /
         weight_decay (e.g. by a scheduler, main.py:104) re-captures the graph."""
+        if self.graph is not None and self._state_key() != self.state_key:
+            self.invalidate()   # parameters / optimizer state changed outside the graph
         self.calls += 1
         if not self.enabled or self.calls <= self.eager_steps:
             return self._eager(batch)

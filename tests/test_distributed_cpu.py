@@ -1,10 +1,11 @@
-"""Data-parallel path on CPU: world_size 2 over gloo.
+"""Data-parallel path on CPU: world_size 2, 4 and 8 over gloo
+(SURVEY.md §4.4).
 
 The product's CLIPModel (mae_clip_amd/CLIP.py) shards the batch across ranks,
 all-gathers the projection embeddings (distributed.gather_rows), scales the
 MAE term by 1/world and SUM-all-reduces gradients (distributed.DataParallel).
 Here the same composition is driven with the oracle's CPU modules so the
-claim "2 ranks x B == 1 rank x 2B, exactly" is checked without a GPU:
+claim "W ranks x B == 1 rank x WB, exactly" is checked without a GPU:
 loss, every parameter gradient and the per-sample MAE masks must match the
 single-process full-batch oracle."""
 import functools
@@ -27,7 +28,7 @@ def _free_port():
 
 def _worker(rank, world, port, fn, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, 4 // world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         out[rank] = fn(rank, world)
@@ -64,12 +65,12 @@ def test_gather_rows_forward_backward():
 B_LOCAL = 3
 
 
-def _model_and_batch():
+def _model_and_batch(world=2):
     from oracle.ref_model import CLIPModel
     torch.manual_seed(0)
     cfg = oracle_config(mask_ratio=0.75)
     m = CLIPModel(cfg).double().eval()   # eval: dropout off, so both sides are deterministic
-    batch = make_batch(2 * B_LOCAL, cfg.img_size, seed=3)
+    batch = make_batch(world * B_LOCAL, cfg.img_size, seed=3)
     batch["image"] = batch["image"].double()
     return m, cfg, batch
 
@@ -92,11 +93,11 @@ def _dp_forward(m, cfg, batch, rank, world):
 
 def _dp_body(bucket_mb, overlap, rank, world, grad_dtype=torch.float32):
         from mae_clip_amd.distributed import DataParallel
-        m, cfg, batch = _model_and_batch()
-        if rank == 1:   # replicas start different; DataParallel broadcasts rank 0's weights
+        m, cfg, batch = _model_and_batch(world)
+        if rank > 0:   # replicas start different; DataParallel broadcasts rank 0's weights
             with torch.no_grad():
                 for p in m.parameters():
-                    p.add_(1.0)
+                    p.add_(float(rank))
         dp = DataParallel(m, bucket_mb=bucket_mb, grad_dtype=grad_dtype)
         dp.overlap = overlap
         sl = slice(rank * B_LOCAL, (rank + 1) * B_LOCAL)
@@ -108,14 +109,15 @@ def _dp_body(bucket_mb, overlap, rank, world, grad_dtype=torch.float32):
         return clip, mae, mask, grads, len(dp.buckets)
 
 
-@pytest.mark.parametrize("bucket_mb,overlap", [(64.0, True), (0.05, True), (0.05, False)])
-def test_data_parallel_equals_full_batch(bucket_mb, overlap):
-    res = run_ranks(functools.partial(_dp_body, bucket_mb, overlap))
-    m, cfg, batch = _model_and_batch()
+@pytest.mark.parametrize("world,bucket_mb,overlap", [(2, 64.0, True), (2, 0.05, True), (2, 0.05, False),
+                                                     (4, 0.05, True), (8, 0.05, True), (8, 64.0, False)])
+def test_data_parallel_equals_full_batch(world, bucket_mb, overlap):
+    res = run_ranks(functools.partial(_dp_body, bucket_mb, overlap), world=world)
+    m, cfg, batch = _model_and_batch(world)
     ref_loss = m(batch, step=0)
     ref_loss.backward()
     ref_clip, ref_mae = m.last_losses["clip"], m.last_losses["mae"]
-    ref_mask = m.mask_for_batch(2 * B_LOCAL, 0, 0)[2]
+    ref_mask = m.mask_for_batch(world * B_LOCAL, 0, 0)[2]
     if bucket_mb < 1:
         assert res[0][4] > 2   # several buckets actually exercised
     for r, (clip, mae, mask, grads, _) in enumerate(res):
@@ -127,10 +129,11 @@ def test_data_parallel_equals_full_batch(bucket_mb, overlap):
                 continue
             assert torch.allclose(grads[n], p.grad, atol=2e-6, rtol=1e-4), n
     # global MAE loss is the mean of the per-rank losses (equal masked counts)
-    assert torch.allclose((res[0][1] + res[1][1]) / 2, ref_mae, atol=1e-6, rtol=1e-5)
-    # both ranks hold identical synchronised gradients
-    for n in res[0][3]:
-        assert torch.equal(res[0][3][n], res[1][3][n]), n
+    assert torch.allclose(sum(r[1] for r in res) / world, ref_mae, atol=1e-6, rtol=1e-5)
+    # every rank holds identical synchronised gradients
+    for r in range(1, world):
+        for n in res[0][3]:
+            assert torch.equal(res[0][3][n], res[r][3][n]), (r, n)
 
 
 def test_grad_arena_slot_handed_out_once():
@@ -159,18 +162,20 @@ def _ragged_body(rank, world):
     return None
 
 
-def test_data_parallel_rejects_ragged_batches():
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_rejects_ragged_batches(world):
     """ranks with different local B fail with a clear error, not a hang."""
-    res = run_ranks(_ragged_body)
+    res = run_ranks(_ragged_body, world=world)
     assert all(r is not None and "different local batch sizes" in r for r in res)
 
 
-def test_data_parallel_bf16_gradient_allreduce():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_data_parallel_bf16_gradient_allreduce(world):
     """opt-in bf16 all-reduce buckets (DataParallel(grad_dtype=bfloat16)): every
     gradient within 1e-2 relative L2 of the fp32 single-process full batch
-    (two bf16 roundings + one bf16 add per element), ranks identical."""
-    res = run_ranks(functools.partial(_dp_body, 0.05, True, grad_dtype=torch.bfloat16))
-    m, cfg, batch = _model_and_batch()
+    (two bf16 roundings + world - 1 bf16 adds per element), ranks identical."""
+    res = run_ranks(functools.partial(_dp_body, 0.05, True, grad_dtype=torch.bfloat16), world=world)
+    m, cfg, batch = _model_and_batch(world)
     m(batch, step=0).backward()
     worst = 0.0
     for n, p in m.named_parameters():
@@ -180,5 +185,20 @@ def test_data_parallel_bf16_gradient_allreduce():
         den = p.grad.double().norm().item()
         if den > 0:
             worst = max(worst, (g - p.grad.double()).norm().item() / den)
-        assert torch.equal(res[0][3][n], res[1][3][n]), n
+        for r in range(1, world):
+            assert torch.equal(res[0][3][n], res[r][3][n]), n
     assert worst < 1e-2, worst
+
+
+def test_grad_arena_slots_are_16b_aligned():
+    """arena slots start on 4-float boundaries, so every all-reduce
+    bucket slice handed to the flat cast kernel is 16-B aligned; the padding
+    is zero."""
+    from mae_clip_amd.distributed import GradArena
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (3, 5, 8, 1, 7)]
+    ar = GradArena(ps, "cpu")
+    offs = [ar.offsets[id(p)][0] for p in ps]
+    assert offs == [0, 4, 12, 20, 24]
+    for p in ps:
+        ar.view(p).fill_(1.0)
+    assert ar.flat.sum().item() == sum(p.numel() for p in ps)

@@ -159,3 +159,47 @@ def test_captured_step_with_rccl_data_parallel(dev):
     assert eager["losses"] == graph["losses"], (eager["losses"], graph["losses"])
     for n, p in eager["params"].items():
         assert torch.equal(p, graph["params"][n]), n
+
+
+def _bf16_reduce_rank(rank, world, port, out):
+    """the opt-in bf16 gradient all-reduce on the device path (the
+    maeclip_cast_flat kernel both ways around an RCCL bf16 SUM). At world 1 the
+    sum is the rank's own gradient, so every gradient must equal the fp32
+    run's gradient rounded to bf16 (deterministic kernels: the two backward
+    passes produce identical fp32 gradients)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        from mae_clip_amd import _lib
+        from mae_clip_amd.distributed import DataParallel
+        from tests.helpers import make_batch
+        _lib.load()
+        res = {}
+        for gd in (torch.float32, torch.bfloat16):
+            m = _model("bf16").train()
+            dp = DataParallel(m, bucket_mb=1.0, grad_dtype=gd)
+            b = {k: v.cuda() for k, v in make_batch(8, 32, seed=3).items()}
+            loss = m(b)
+            loss.backward()
+            dp.sync_gradients()
+            torch.cuda.synchronize()
+            res[str(gd)] = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters() if p.grad is not None}
+            res[str(gd) + "_buckets"] = len(dp.buckets)
+            res[str(gd) + "_offsets"] = [o for o, _, _ in dp.arena.offsets.values()]
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bf16_gradient_allreduce_rccl_world1(dev):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bf16_reduce_rank, args=(1, _free_port(), out), nprocs=1, join=True)
+    r = out[0]
+    f32, b16 = r[str(torch.float32)], r[str(torch.bfloat16)]
+    assert r[str(torch.bfloat16) + "_buckets"] > 1
+    assert all(o % 4 == 0 for o in r[str(torch.bfloat16) + "_offsets"])   # 16-B aligned slots
+    assert set(f32) == set(b16) and len(f32) > 10
+    for n, g in f32.items():
+        assert torch.equal(b16[n], g.to(torch.bfloat16).float()), n

@@ -248,7 +248,7 @@ def _clip_ref64(I, T, tau):
     return ref.item(), I64.grad, T64.grad
 
 
-@pytest.mark.parametrize("N", [1, 3, 5, 7, 8, 64, 100, 256, 1024, 2048])
+@pytest.mark.parametrize("N", [1, 3, 5, 7, 8, 64, 100, 256, 1024, 2048, 2500, 4100])
 @pytest.mark.parametrize("tau", [1.0, 0.5])
 def test_clip_loss_kernel_vs_torch(dev, N, tau):
     """Fused CLIP loss (no N x N in HBM) vs fp64 autograd of the reference
@@ -267,7 +267,8 @@ def test_clip_loss_kernel_vs_torch(dev, N, tau):
     assert torch.equal(loss, loss2) and torch.equal(dI, dI2) and torch.equal(dT, dT2)
 
 
-@pytest.mark.parametrize("N,rows", [(2048, (256, 256)), (1024, (896, 128)), (100, (37, 50)), (256, (0, 256))])
+@pytest.mark.parametrize("N,rows", [(2048, (256, 256)), (1024, (896, 128)), (100, (37, 50)), (256, (0, 256)),
+                                    (2500, (2100, 400)), (4100, (0, 2048)), (4100, (4000, 100))])
 def test_clip_loss_gradient_rows(dev, N, rows):
     """Data-parallel form: every rank evaluates the loss of the gathered batch
     and asks for the gradient of its own row slice only -- equal to that slice
@@ -690,3 +691,29 @@ def test_uint8_pixels_fused_into_gather_and_mae_targets(dev, dtype, geo):
         d1, c1 = K.mae_loss_bwd(pred, px, mask, p, norm_pix, gl, float(mask.sum().item()))
         d2, c2 = K.mae_loss_bwd(pred, img, mask, p, norm_pix, gl, float(mask.sum().item()))
         assert torch.equal(d1, d2) and torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 7, 1023, 4097, 65539])
+@pytest.mark.parametrize("direction", ["f32_bf16", "bf16_f32"])
+def test_cast_flat_odd_sizes(dev, n, direction):
+    """maeclip_cast_flat (the bf16 gradient all-reduce's bucket casts) at odd
+    sizes and vector tails, at an odd 16-B-aligned start offset inside a
+    buffer (a bucket slice of the GradArena): RNE f32 -> bf16 like torch,
+    exact bf16 -> f32, scale applied, nothing written past n."""
+    torch.manual_seed(n)
+    base = torch.randn(n + 8, device=dev) * 3.0
+    if direction == "f32_bf16":
+        src = base[4:4 + n]
+        dst_buf = torch.full((n + 8,), 7.0, device=dev, dtype=torch.bfloat16)
+        dst = dst_buf[4:4 + n]
+        K.cast_flat(src, dst, scale=0.5)
+        ref = (src * 0.5).to(torch.bfloat16)
+    else:
+        src = base.to(torch.bfloat16)[4:4 + n]
+        dst_buf = torch.full((n + 8,), 7.0, device=dev)
+        dst = dst_buf[4:4 + n]
+        K.cast_flat(src, dst, scale=2.0)
+        ref = src.float() * 2.0
+    torch.cuda.synchronize()
+    assert torch.equal(dst, ref)
+    assert (dst_buf[:4] == 7.0).all() and (dst_buf[4 + n:] == 7.0).all()
