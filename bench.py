@@ -92,6 +92,25 @@ def parity_c0(device):
     return abs(lp - lr), lp, lr
 
 
+def parity_headline(device, precision="bf16", B=4):
+    """|loss(product) - loss(CPU oracle, fp64)| at the metric's own model shapes
+    and precision: ViT-B/16 @224, mask .75, 8x512 decoder, 6-layer text (the C2
+    step this bench times), bf16, B=4 (the oracle is a CPU fp64 restatement of
+    CLIP.py:34-43 + modules.py, so B is kept small), forward in eval mode."""
+    sys.path.insert(0, ROOT)
+    from tests.helpers import build_pair, make_batch
+    kw = dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6, mask_ratio=0.75,
+              decoder_embed_dim=512, decoder_depth=8, decoder_num_heads=16)
+    prod, ref = build_pair(precision, **kw)
+    prod.eval()
+    ref.eval()
+    b = make_batch(B, 224, seed=12)
+    with torch.no_grad():
+        lp = prod({k: v.to(device) for k, v in b.items()}).item()
+        lr = ref(dict(b, image=b["image"].double())).item()
+    return abs(lp - lr), abs(lp - lr) / max(1.0, abs(lr)), lp, lr
+
+
 def cpu_model_name():
     try:
         for line in open("/proc/cpuinfo"):
@@ -501,6 +520,16 @@ def main():
                                             "config": "C0 ViT-Tiny/16@32, 2-layer text, mask .75, B=8, fp32"}
             except Exception as e:  # reported, never hides the perf line
                 out["loss_delta_vs_ref"] = {"error": repr(e)}
+            if args.config == "c2":
+                try:
+                    t0 = time.time()
+                    da, dr, lp, lr = parity_headline(device, args.precision)
+                    out["loss_delta_vs_ref_headline"] = {
+                        "abs": da, "rel": dr, "product": lp, "oracle": lr, "precision": args.precision,
+                        "config": "C2 model shapes (ViT-B/16@224, mask .75, 8x512 decoder, 6-layer text), B=4, "
+                                  "eval-mode forward vs the fp64 CPU oracle", "seconds": round(time.time() - t0, 1)}
+                except Exception as e:
+                    out["loss_delta_vs_ref_headline"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         sys.stdout.flush()

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 5
+#define MAECLIP_ABI_VERSION 6
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -285,9 +285,11 @@ int32_t maeclip_pool_bwd(const float* dout, int32_t B, int32_t n, int32_t D, flo
 /* nn.Dropout with the library's counter-based mask (same as LN in_dropout) */
 int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t D, int64_t ld, float p, uint64_t seed,
                         const int64_t* step_ptr, void* stream);
-/* DistilBERT Embeddings word+position gather (modeling_distilbert.py:92-117) */
+/* DistilBERT Embeddings word+position gather (modeling_distilbert.py:92-117);
+ * mask_in (optional, int64 [B*T], the tokenizer's attention_mask) -> mask_out
+ * (f32 [B*T], the attention kernels' key mask) in the same launch */
 int32_t maeclip_embed_fwd(const int64_t* ids, const float* word, const float* pos, int32_t B, int32_t T, int32_t D,
-                          int64_t V, float* out, void* stream);
+                          int64_t V, float* out, const int64_t* mask_in, float* mask_out, void* stream);
 
 /* ---------------------------------------------------------- multi-tensor */
 typedef struct {
@@ -504,6 +506,18 @@ int32_t maeclip_clip_loss(const maeclip_clip_args* args, void* stream);
  * whole training step can be captured once in a HIP graph and replayed. */
 #define MAECLIP_STEP_MULT 0x9E3779B97F4A7C15ull
 int32_t maeclip_counter_add(int64_t* counter, int64_t delta, void* stream);
+/* snap[0] = counter[0]; counter[0] += delta -- the step a forward used, kept for
+ * its backward (dropout masks re-drawn there) without a separate copy */
+int32_t maeclip_counter_add_snap(int64_t* counter, int64_t delta, int64_t* snap, void* stream);
+/* loss combination on device scalars (CLIP.py total loss + MAE term):
+ * out[0] = a[0] + w * b[0] */
+int32_t maeclip_scalar_axpy(const float* a, const float* b, float w, float* out, void* stream);
+/* dst_i[k] = w * s[0] * src_i[k] (src_i NULL: w * s[0]) for two dense f32
+ * arrays in one launch (n_i = 0: unused); src_i == dst_i allowed. The
+ * backward of a loss that scales stored gradients by the incoming grad_output
+ * (a device scalar) without a host sync. */
+int32_t maeclip_scale_by_scalar2(const float* src0, float* dst0, int64_t n0, const float* src1, float* dst1, int64_t n1,
+                                 const float* s, float w, void* stream);
 /* stream-ordered device timestamp (REALTIME counter, maeclip_wallclock_khz ticks/ms) */
 int32_t maeclip_timestamp(int64_t* dst, void* stream);
 int64_t maeclip_wallclock_khz(void);

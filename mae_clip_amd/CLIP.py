@@ -59,6 +59,10 @@ class CLIPModel(nn.Module):
         # captured HIP graph of the step (mae_clip_amd.graph) draws fresh masks
         # on every replay. Not persistent: state_dict keys stay the reference's.
         self.register_buffer("step_counter", torch.zeros(1, dtype=torch.int64), persistent=False)
+        # step_snaps[s % 8]: the step_counter value training forward s ran with,
+        # written by the kernel that advances the counter; that forward's
+        # backward re-draws its dropout masks from it (up to 8 forwards in flight)
+        self.register_buffer("step_snaps", torch.zeros(8, dtype=torch.int64), persistent=False)
         self.last_losses = {}
         self.process_group = None
         self.grad_arena = None     # set by distributed.DataParallel (flat all-reduce buffer)
@@ -134,8 +138,9 @@ class CLIPModel(nn.Module):
         else:
             text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17,
                                               dtype=dtype, step_ptr=sc)
-        image_embeddings = self.image_projection(feat, seed=seed + 29, step_ptr=sc)
-        text_embeddings = self.text_projection(text_features, seed=seed + 31, step_ptr=sc)
+        snap = self.step_snaps[self.step % 8:self.step % 8 + 1] if self.training else None
+        image_embeddings = self.image_projection(feat, seed=seed + 29, step_ptr=sc, bwd_step_ptr=snap)
+        text_embeddings = self.text_projection(text_features, seed=seed + 31, step_ptr=sc, bwd_step_ptr=snap)
         clip = clip_loss(image_embeddings, text_embeddings, self.temperature,
                          group=self.process_group if world > 1 else None)
         loss = clip
@@ -163,11 +168,11 @@ class CLIPModel(nn.Module):
                                         dec.decoder_norm.weight, dec.decoder_norm.bias, dec.decoder_pred.weight,
                                         dec.decoder_pred.bias)
             self.last_losses["mae"] = ml.detach()
-            loss = clip + self.mae_weight * ml
+            loss = Fn.CombineLossFn.apply(clip, ml, self.mae_weight)
             self.last_mask = (ids_shuffle, ids_restore, mask)
         if self.training:
+            K.counter_add_snap(sc, snap, 1)
             self.step += 1
-            K.counter_add(sc, 1)
         return loss
 
 

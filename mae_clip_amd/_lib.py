@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -172,7 +172,7 @@ _SIGS = {
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),
     "maeclip_pool_bwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp]),
     "maeclip_dropout": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i64, c_f32, c_u64, c_vp, c_vp]),
-    "maeclip_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp]),
+    "maeclip_embed_fwd": (c_i32, [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "maeclip_mt_chunk": (c_i64, []),
     "maeclip_colsum_multi": (c_i32, [c_vp, C.POINTER(ColsumEntry), c_i32, c_vp]),
     "maeclip_cast_multi": (c_i32, [c_vp, C.POINTER(MtEntry), c_i32, c_vp]),
@@ -190,6 +190,9 @@ _SIGS = {
     "maeclip_clip_loss_workspace": (c_sz, [c_i64, c_i64, c_i64]),
     "maeclip_clip_loss": (c_i32, [C.POINTER(ClipArgs), c_vp]),
     "maeclip_counter_add": (c_i32, [c_vp, c_i64, c_vp]),
+    "maeclip_counter_add_snap": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "maeclip_scalar_axpy": (c_i32, [c_vp, c_vp, C.c_float, c_vp, c_vp]),
+    "maeclip_scale_by_scalar2": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, C.c_float, c_vp]),
     "maeclip_memcpy_h2d": (c_i32, [c_vp, c_vp, c_sz, c_vp]),
     "maeclip_timestamp": (c_i32, [c_vp, c_vp]),
     "maeclip_wallclock_khz": (c_i64, []),

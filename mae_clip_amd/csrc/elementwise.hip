@@ -128,9 +128,11 @@ __global__ void __launch_bounds__(NTH) dropout_kernel(const float* __restrict__ 
 // out[b*T+t] = word[ids[b,t]] + pos[t]
 __global__ void __launch_bounds__(NTH) embed_kernel(const int64_t* __restrict__ ids, const float* __restrict__ word,
                                                     const float* __restrict__ pos, int T, int D, int64_t V,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ out, const int64_t* __restrict__ mask_in,
+                                                    float* __restrict__ mask_out) {
   const int64_t row = blockIdx.y;
   const int d = (blockIdx.x * NTH + threadIdx.x) * 4;
+  if (mask_out && d == 0) mask_out[row] = (float)mask_in[row];
   if (d >= D) return;
   int64_t id = ids[row];
   id = id < 0 ? 0 : (id >= V ? V - 1 : id);
@@ -421,10 +423,12 @@ extern "C" int32_t maeclip_dropout(const float* x, float* y, int64_t M, int32_t 
 }
 
 extern "C" int32_t maeclip_embed_fwd(const int64_t* ids, const float* word, const float* pos, int32_t B, int32_t T,
-                                     int32_t D, int64_t V, float* out, void* stream) {
+                                     int32_t D, int64_t V, float* out, const int64_t* mask_in, float* mask_out,
+                                     void* stream) {
   MC_CHECK_ARG(ids && word && pos && out && D % 4 == 0, "maeclip_embed_fwd: bad args");
+  MC_CHECK_ARG((mask_in == nullptr) == (mask_out == nullptr), "maeclip_embed_fwd: mask_in and mask_out go together");
   hipLaunchKernelGGL(embed_kernel, dim3((D / 4 + NTH - 1) / NTH, (unsigned)(B * T)), dim3(NTH), 0, (hipStream_t)stream, ids,
-                     word, pos, T, D, V, out);
+                     word, pos, T, D, V, out, mask_in, mask_out);
   MC_CHECK_LAUNCH("maeclip_embed_fwd");
   return 0;
 }
@@ -450,14 +454,63 @@ extern "C" int32_t maeclip_adamw_multi(const maeclip_mt_entry* dev_entries, cons
 }
 
 namespace {
-__global__ void counter_add_kernel(int64_t* c, int64_t delta) {
-  if (threadIdx.x == 0) *c += delta;
+__global__ void counter_add_kernel(int64_t* c, int64_t delta, int64_t* snap) {
+  if (threadIdx.x == 0) {
+    const int64_t v = *c;
+    if (snap) *snap = v;
+    *c = v + delta;
+  }
+}
+__global__ void scalar_axpy_kernel(const float* a, const float* b, float w, float* out) {
+  if (threadIdx.x == 0) out[0] = fmaf(w, b[0], a[0]);
+}
+__global__ void __launch_bounds__(NTH) scale2_kernel(const float* __restrict__ s0, float* __restrict__ d0, int64_t n0,
+                                                     const float* __restrict__ s1, float* __restrict__ d1, int64_t n1,
+                                                     const float* __restrict__ sc, float w, int64_t nb0) {
+  const float f = w * sc[0];
+  const bool second = blockIdx.x >= nb0;
+  const float* src = second ? s1 : s0;
+  float* dst = second ? d1 : d0;
+  const int64_t n = second ? n1 : n0;
+  const int64_t i = ((second ? blockIdx.x - nb0 : blockIdx.x) * (int64_t)NTH + threadIdx.x) * 4;
+  if (i + 3 < n && ((((uintptr_t)dst) | ((uintptr_t)(src ? src : dst))) & 15) == 0) {
+    const v4f v = src ? *(const v4f*)(src + i) : v4f{1.f, 1.f, 1.f, 1.f};
+    *(v4f*)(dst + i) = v * f;
+  } else {
+    for (int64_t j = i; j < n && j < i + 4; ++j) dst[j] = (src ? src[j] : 1.f) * f;
+  }
 }
 }  // namespace
 
+extern "C" int32_t maeclip_counter_add_snap(int64_t* counter, int64_t delta, int64_t* snap, void* stream) {
+  MC_CHECK_ARG(counter != nullptr && snap != nullptr, "maeclip_counter_add_snap: null pointer");
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta, snap);
+  MC_CHECK_LAUNCH("maeclip_counter_add_snap");
+  return 0;
+}
+
+extern "C" int32_t maeclip_scalar_axpy(const float* a, const float* b, float w, float* out, void* stream) {
+  MC_CHECK_ARG(a && b && out, "maeclip_scalar_axpy: null pointer");
+  hipLaunchKernelGGL(scalar_axpy_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, w, out);
+  MC_CHECK_LAUNCH("maeclip_scalar_axpy");
+  return 0;
+}
+
+extern "C" int32_t maeclip_scale_by_scalar2(const float* src0, float* dst0, int64_t n0, const float* src1, float* dst1,
+                                            int64_t n1, const float* s, float w, void* stream) {
+  MC_CHECK_ARG(s != nullptr && n0 >= 0 && n1 >= 0 && (n0 == 0 || dst0) && (n1 == 0 || dst1),
+               "maeclip_scale_by_scalar2: bad args");
+  const int64_t nb0 = (n0 + 4 * NTH - 1) / (4 * NTH), nb1 = (n1 + 4 * NTH - 1) / (4 * NTH);
+  if (nb0 + nb1 == 0) return 0;
+  hipLaunchKernelGGL(scale2_kernel, dim3((unsigned)(nb0 + nb1)), dim3(NTH), 0, (hipStream_t)stream, src0, dst0, n0, src1,
+                     dst1, n1, s, w, nb0);
+  MC_CHECK_LAUNCH("maeclip_scale_by_scalar2");
+  return 0;
+}
+
 extern "C" int32_t maeclip_counter_add(int64_t* counter, int64_t delta, void* stream) {
   MC_CHECK_ARG(counter != nullptr, "maeclip_counter_add: null counter");
-  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta);
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, delta, (int64_t*)nullptr);
   MC_CHECK_LAUNCH("maeclip_counter_add");
   return 0;
 }

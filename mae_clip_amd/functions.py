@@ -465,6 +465,7 @@ class ProjSpec:
     p_drop: float
     seed: int
     step_ptr: torch.Tensor = None   # device step counter (dropout mask of the current step)
+    bwd_step_ptr: torch.Tensor = None   # the same step's value as the backward will find it (snapshot slot)
 
 
 class ProjectionHeadFn(torch.autograd.Function):
@@ -486,7 +487,9 @@ class ProjectionHeadFn(torch.autograd.Function):
         ctx.spec = spec
         # the step counter advances at the end of the forward: the backward
         # re-draws this forward's dropout mask from a snapshot of the step
-        ctx.step_snap = spec.step_ptr.clone() if (spec.step_ptr is not None and spec.p_drop > 0) else None
+        ctx.step_snap = None
+        if spec.step_ptr is not None and spec.p_drop > 0:
+            ctx.step_snap = spec.bwd_step_ptr if spec.bwd_step_ptr is not None else spec.step_ptr.clone()
         return out
 
     @staticmethod
@@ -540,4 +543,22 @@ class ClipLossFn(torch.autograd.Function):
     def backward(ctx, gl):
         dI, dT = ctx.grads
         ctx.grads = None
-        return dI * gl, dT * gl, None, None
+        # scaled in place by the device grad_output: one launch, no host sync
+        K.scale_by_scalar(gl.reshape(1).contiguous(), 1.0, dI, dT, dI, dT)
+        return dI, dT, None, None
+
+
+class CombineLossFn(torch.autograd.Function):
+    """loss = clip + w * mae on device scalars (one launch; backward: grad_output
+    to the CLIP term as is, w * grad_output to the MAE term in one launch)."""
+
+    @staticmethod
+    def forward(ctx, clip, mae, w):
+        ctx.w = float(w)
+        return K.scalar_axpy(clip, mae, w)
+
+    @staticmethod
+    def backward(ctx, gl):
+        g = gl.reshape(1).contiguous()
+        gm, _ = K.scale_by_scalar(g, ctx.w, out_x=torch.empty((), device=g.device, dtype=torch.float32))
+        return gl, gm, None

@@ -93,9 +93,12 @@ class CapturedStep:
         self.opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        # backward seed allocated outside the graph: loss.backward() would fill
+        # a fresh ones tensor inside every replay
+        one = torch.ones((), device=next(self.model.parameters()).device, dtype=torch.float32)
         with torch.cuda.graph(g, capture_error_mode="relaxed"):
             loss = self.model(self.static)
-            loss.backward()
+            torch.autograd.backward(loss, grad_tensors=one.expand_as(loss) if loss.dim() else one)
             if self.dp is not None:
                 self.dp.sync_gradients()
             self.opt.step()
@@ -107,6 +110,7 @@ class CapturedStep:
         # later eager fallback steps or a re-capture (torch's AccumulateGrad
         # stream-mismatch hazard); the replays still refresh its storage
         self.graph, self.loss = g, loss.detach()
+        self._seed = one
         self.hp_key = self._hparams()
         self.graph_grads = [(p, p.grad) for grp in self.opt.param_groups for p in grp["params"]]
         self.state_key = self._state_key()

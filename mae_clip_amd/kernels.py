@@ -328,13 +328,23 @@ def dropout(x, p, seed, out=None, step_ptr=None):
     return out
 
 
-def embed_fwd(ids, word, pos):
+def embed_fwd(ids, word, pos, mask=None):
+    """word + position embedding rows [B*T, D] (f32). mask (optional, int64
+    [B, T] attention_mask): also returns it as the f32 key mask [B, T],
+    converted in the same launch."""
     _dev(ids, word, pos)
     B, T = ids.shape
     V, D = word.shape
     out = torch.empty((B * T, D), device=word.device, dtype=torch.float32)
-    _call("maeclip_embed_fwd", ids.data_ptr(), word.data_ptr(), pos.data_ptr(), B, T, D, V, out.data_ptr(), _stream())
-    return out
+    mo = None
+    if mask is not None:
+        _dev(mask)
+        if mask.dtype != torch.int64 or mask.shape != (B, T) or not mask.is_contiguous():
+            raise ValueError("embed_fwd: mask must be a dense int64 [B, T] tensor")
+        mo = torch.empty((B, T), device=word.device, dtype=torch.float32)
+    _call("maeclip_embed_fwd", ids.data_ptr(), word.data_ptr(), pos.data_ptr(), B, T, D, V, out.data_ptr(),
+          _ptr(mask), _ptr(mo), _stream())
+    return out if mask is None else (out, mo)
 
 
 # -------------------------------------------------------------- LayerNorm
@@ -572,6 +582,41 @@ def clip_loss(I, T, temperature, want_grad=True, grad_rows=None, row_loss=False)
 
 
 # ------------------------------------------------------------ multi-tensor
+def counter_add_snap(counter, snap, delta=1):
+    """snap[0] = counter[0]; counter[0] += delta (stream-ordered, one launch)."""
+    _dev(counter, snap)
+    _call("maeclip_counter_add_snap", counter.data_ptr(), int(delta), snap.data_ptr(), _stream())
+
+
+def scalar_axpy(a, b, w):
+    """a + w * b on device f32 scalars (no host sync)."""
+    _dev(a, b)
+    out = torch.empty((), device=a.device, dtype=torch.float32)
+    _call("maeclip_scalar_axpy", a.data_ptr(), b.data_ptr(), float(w), out.data_ptr(), _stream())
+    return out
+
+
+def scale_by_scalar(s, w=1.0, x=None, y=None, out_x=None, out_y=None):
+    """(w * s[0]) * x and (w * s[0]) * y in one launch (s: device f32 scalar;
+    x None: the constant 1, then out_x must be given). Returns (out_x, out_y)."""
+    _dev(s)
+    def prep(src, dst):
+        if src is None and dst is None:
+            return None, None, 0
+        if src is not None:
+            _dev(src)
+            if src.dtype != torch.float32 or not src.is_contiguous():
+                raise ValueError("scale_by_scalar: dense f32 tensors")
+            if dst is None:
+                dst = torch.empty_like(src)
+        return src, dst, dst.numel()
+    x, out_x, nx = prep(x, out_x)
+    y, out_y, ny = prep(y, out_y)
+    _call("maeclip_scale_by_scalar2", _ptr(x), _ptr(out_x), nx, _ptr(y), _ptr(out_y), ny, s.data_ptr(), float(w),
+          _stream())
+    return out_x, out_y
+
+
 def counter_add(counter, delta=1):
     """counter (device int64[1]) += delta, stream-ordered (graph-capturable)."""
     _dev(counter)
@@ -586,24 +631,39 @@ class PinnedStager:
     """Host -> device staging of small descriptor arrays through a ring of pinned
     buffers; a buffer is reused only after the async copy that read it is done.
 
-    Under HIP-graph capture the copy becomes a memcpy node that re-reads its
-    pinned source at every replay, so each captured stage gets a pinned buffer
-    of its own that is never rewritten (kept in `captured` for the graph's life)."""
+    Under HIP-graph capture the descriptors of a stage are constants of the
+    graph (every pointer in them is fixed for its life), so they are uploaded
+    ONCE, at capture time, on an uncaptured upload stream into a device buffer
+    kept in `captured` for the graph's life: the graph holds no memcpy node
+    and a replay copies nothing."""
 
     def __init__(self, slots=4):
         self.bufs = [None] * slots
         self.events = [None] * slots
         self.k = 0
         self.captured = []
+        self.upload = {}
+
+    def _upload_stream(self, device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        s = self.upload.get(idx)
+        if s is None:
+            s = self.upload[idx] = torch.cuda.Stream(device=idx)
+        return s
 
     def stage(self, host_struct_array, device):
         nbytes = C.sizeof(host_struct_array)
         if _capturing():
             pin = torch.empty(max(nbytes, 16), dtype=torch.uint8).pin_memory()
             pin[:nbytes].numpy()[:] = memoryview(host_struct_array).cast("B")
-            dev = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
-            _call("maeclip_memcpy_h2d", dev.data_ptr(), pin.data_ptr(), nbytes, _stream())
-            self.captured.append(pin)
+            up = self._upload_stream(device)
+            # allocated and filled on the upload stream: outside the capture (and
+            # its private pool), finished before the captured kernels can run
+            with torch.cuda.stream(up):
+                dev = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+                _call("maeclip_memcpy_h2d", dev.data_ptr(), pin.data_ptr(), nbytes, up.cuda_stream)
+            up.synchronize()
+            self.captured.append((pin, dev))
             return dev
         k = self.k
         self.k = (k + 1) % len(self.bufs)

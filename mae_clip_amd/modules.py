@@ -452,9 +452,14 @@ class DistilBertModel(nn.Module):
         padrop = self.attn_dropout_p if train else 0.0
         bf = dtype == torch.bfloat16
         ids = input_ids.to(torch.int64).contiguous()
-        am = attention_mask.to(device=input_ids.device, dtype=torch.float32).contiguous()
         emb = self.embeddings
-        x = K.embed_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight)
+        if attention_mask.dtype == torch.int64 and attention_mask.is_contiguous() \
+                and attention_mask.device == input_ids.device:
+            # the tokenizer's int64 mask -> the f32 key mask inside the embedding launch
+            x, am = K.embed_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight, mask=attention_mask)
+        else:
+            am = attention_mask.to(device=input_ids.device, dtype=torch.float32).contiguous()
+            x = K.embed_fwd(ids, emb.word_embeddings.weight, emb.position_embeddings.weight)
         h, _, _, hT, _ = K.ln_fwd(x, emb.LayerNorm.weight, emb.LayerNorm.bias, 1e-12, out_dtype=torch.float32,
                                   out_dropout=pdrop, seed_out=seed * 131 + 1, want_stats=False, y2=bf,
                                   step_ptr=step_ptr)
@@ -512,10 +517,13 @@ class ProjectionHead(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.layer_norm = nn.LayerNorm(projection_dim)
 
-    def forward(self, x, seed=0, step_ptr=None):
+    def forward(self, x, seed=0, step_ptr=None, bwd_step_ptr=None):
+        """step_ptr: device step counter keying the dropout mask; bwd_step_ptr:
+        where that step's value will be when the backward runs (CLIPModel's
+        snapshot slot; None: the backward keeps a copy of it)."""
         _require_device(x, "projection input")
         p = self.dropout.p if self.training else 0.0
-        spec = Fn.ProjSpec(p_drop=p, seed=seed, step_ptr=step_ptr)
+        spec = Fn.ProjSpec(p_drop=p, seed=seed, step_ptr=step_ptr, bwd_step_ptr=bwd_step_ptr)
         return Fn.ProjectionHeadFn.apply(x, spec, self.projection.weight, self.projection.bias, self.fc.weight,
                                          self.fc.bias, self.layer_norm.weight, self.layer_norm.bias)
 

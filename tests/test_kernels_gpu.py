@@ -717,3 +717,57 @@ def test_cast_flat_odd_sizes(dev, n, direction):
     torch.cuda.synchronize()
     assert torch.equal(dst, ref)
     assert (dst_buf[:4] == 7.0).all() and (dst_buf[4 + n:] == 7.0).all()
+
+
+def test_small_step_kernels(dev):
+    """ABI v6 step helpers that replace torch kernels inside the captured step:
+    the counter snapshot, the loss combination and the scaling of stored
+    gradients by a device grad_output; the embedding launch's mask convert."""
+    c = torch.tensor([41], device=dev, dtype=torch.int64)
+    snap = torch.zeros(3, device=dev, dtype=torch.int64)
+    K.counter_add_snap(c, snap[1:2], 1)
+    assert c.item() == 42 and snap.tolist() == [0, 41, 0]
+    a = torch.tensor(1.25, device=dev)
+    b = torch.tensor(-3.5, device=dev)
+    assert K.scalar_axpy(a, b, 0.5).item() == 1.25 - 1.75
+    s = torch.tensor([0.75], device=dev)
+    for n0, n1 in [(65536, 65536), (5, 0), (1023, 4097), (0, 3)]:
+        x = torch.randn(n0, device=dev)
+        y = torch.randn(n1, device=dev)
+        ox, oy = K.scale_by_scalar(s, 2.0, x if n0 else None, y if n1 else None,
+                                   out_x=None, out_y=None) if n0 and n1 else (None, None)
+        if n0 and n1:
+            assert torch.equal(ox, x * 1.5) and torch.equal(oy, y * 1.5)
+        # in place
+        x2, y2 = x.clone(), y.clone()
+        K.scale_by_scalar(s, 1.0, x2 if n0 else None, y2 if n1 else None, x2 if n0 else None, y2 if n1 else None)
+        assert torch.equal(x2, x * 0.75) and torch.equal(y2, y * 0.75)
+    one = torch.empty((), device=dev)
+    out, _ = K.scale_by_scalar(s, 4.0, out_x=one)
+    assert out.item() == 3.0
+    ids = torch.randint(0, 100, (3, 7), device=dev)
+    word = torch.randn(100, 64, device=dev)
+    pos = torch.randn(7, 64, device=dev)
+    m = torch.randint(0, 2, (3, 7), device=dev)
+    e, mf = K.embed_fwd(ids, word, pos, mask=m)
+    assert torch.equal(mf, m.float())
+    assert torch.equal(e, (word[ids] + pos[None]).reshape(21, 64))
+
+
+def test_combined_loss_backward_matches_torch(dev):
+    """CombineLossFn / ClipLossFn backward (device-scalar scaling kernels) ==
+    torch autograd of clip + w * mae with a non-unit grad_output."""
+    from mae_clip_amd import functions as Fn
+    clip = torch.tensor(2.0, device=dev, requires_grad=True)
+    mae = torch.tensor(0.5, device=dev, requires_grad=True)
+    loss = Fn.CombineLossFn.apply(clip, mae, 0.3)
+    assert abs(loss.item() - 2.15) < 1e-6
+    loss.backward(torch.tensor(2.0, device=dev))
+    assert clip.grad.item() == 2.0 and abs(mae.grad.item() - 0.6) < 1e-7
+    I = torch.nn.functional.layer_norm(torch.randn(16, 256, device=dev), (256,)).requires_grad_()
+    T = torch.nn.functional.layer_norm(torch.randn(16, 256, device=dev), (256,)).requires_grad_()
+    l = Fn.ClipLossFn.apply(I, T, 1.0, None)
+    l.backward(torch.tensor(3.0, device=dev))
+    _, dI, dT = K.clip_loss(I.detach(), T.detach(), 1.0)
+    assert torch.allclose(I.grad, 3.0 * dI, rtol=1e-6, atol=1e-9)
+    assert torch.allclose(T.grad, 3.0 * dT, rtol=1e-6, atol=1e-9)
