@@ -73,7 +73,7 @@ side_stream = True         # frozen text tower || image encoder; weight-gradient
 # bucketed all-reduce when its backward returns; the backward ends with the
 # BOTTOM chunk, whose all-reduce cannot overlap any backward work, so it is
 # the smallest (modules.chunk_bounds).
-dp_encoder_chunk = (2, 4, 6)
+dp_encoder_chunk = (1, 2, 3, 6)
 dp_decoder_chunk = 4       # data parallel: decoder blocks per autograd Function (overlapped by the encoder backward)
 dp_grad_dtype = "fp32"     # data parallel gradient all-reduce: "fp32" (exact) or "bf16" (opt-in, half the bytes)
 wgrad_grouped = True       # all weight gradients of a stack in one grouped GEMM launch (maeclip_wgrad_grouped)

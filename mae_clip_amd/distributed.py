@@ -165,7 +165,7 @@ class DataParallel:
     backward of the earlier layers is still running.
     """
 
-    def __init__(self, model, group=None, bucket_mb=64.0, broadcast=True, grad_dtype=torch.float32):
+    def __init__(self, model, group=None, bucket_mb=64.0, broadcast=True, grad_dtype=torch.float32, tail_mb=32.0):
         """grad_dtype=torch.bfloat16 (opt-in): each bucket is cast to bf16, SUM-
         all-reduced in bf16 (half the xGMI bytes: 225 instead of 449 MB per step
         at ViT-B MAE+CLIP) and cast back into the fp32 arena; the sum carries
@@ -192,18 +192,24 @@ class DataParallel:
         self.arena = GradArena(order, self.params[0].device)
         if hasattr(model, "grad_arena"):
             model.grad_arena = self.arena
-        # buckets = contiguous arena ranges in reverse registration order
+        # buckets = contiguous arena ranges in reverse registration order, cut
+        # from the END of the arena: the last bucket holds the gradients the
+        # backward produces last (the bottom encoder chunk and the patch
+        # embedding), whose all-reduce no later backward work can hide, so it
+        # is capped at tail_mb; the others at bucket_mb
         cap = int(bucket_mb * 2 ** 20)
-        self.buckets, cur, size = [], [], 0
-        for p in order:
+        tcap = int(min(tail_mb, bucket_mb) * 2 ** 20)
+        rev, cur, size = [], [], 0
+        for p in reversed(order):
             nb = p.numel() * 4
-            if cur and size + nb > cap:
-                self.buckets.append(cur)
+            if cur and size + nb > (tcap if not rev else cap):
+                rev.append(cur[::-1])
                 cur, size = [], 0
             cur.append(p)
             size += nb
         if cur:
-            self.buckets.append(cur)
+            rev.append(cur[::-1])
+        self.buckets = rev[::-1]
         self.ranges = []
         for b in self.buckets:
             o0 = self.arena.offsets[id(b[0])][0]

@@ -202,3 +202,24 @@ def test_grad_arena_slots_are_16b_aligned():
     for p in ps:
         ar.view(p).fill_(1.0)
     assert ar.flat.sum().item() == sum(p.numel() for p in ps)
+
+
+def _bucket_body(rank, world):
+    from mae_clip_amd.distributed import DataParallel
+    m, cfg, batch = _model_and_batch(world)
+    dp = DataParallel(m, bucket_mb=0.05, tail_mb=0.01)
+    sizes = [sum(p.numel() * 4 for p in b) for b in dp.buckets]
+    flat = [id(p) for b in dp.buckets for p in b]
+    order = [id(p) for p in reversed([p for p in m.parameters() if p.requires_grad])]
+    one = max(p.numel() * 4 for p in dp.buckets[-1])
+    return sizes, flat == order, one
+
+
+def test_data_parallel_tail_bucket_is_small():
+    """The last all-reduce bucket (the gradients the backward produces last:
+    bottom encoder block + patch embedding, exposed after the backward) is cut
+    at tail_mb; buckets still cover every parameter once, in arena order."""
+    (sizes, ordered, one), = run_ranks(_bucket_body, world=1)
+    assert ordered
+    assert sizes[-1] <= max(0.01 * 2 ** 20, one)
+    assert max(sizes[:-1]) > 0.01 * 2 ** 20

@@ -163,5 +163,6 @@ def test_chunk_bounds():
     assert chunk_bounds(12, None) == [(0, 12)]
     assert chunk_bounds(12, 6) == [(0, 6), (6, 12)]
     assert chunk_bounds(12, (2, 4, 6)) == [(0, 2), (2, 6), (6, 12)]
+    assert chunk_bounds(12, (1, 2, 3, 6)) == [(0, 1), (1, 3), (3, 6), (6, 12)]
     assert chunk_bounds(8, (2, 4, 6)) == [(0, 2), (2, 6), (6, 8)]
     assert chunk_bounds(5, (2,)) == [(0, 2), (2, 4), (4, 5)]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU session script: GPU tests, smoke, default bench, optional extra
+# GPU session script (rounds 3-4): GPU tests, smoke, default bench, optional extra
 # steps selected by $STEPS (space-separated: gemmcal prof). Every GPU step has
 # its own limit and the chain stops at the first failure.
 set -o pipefail
@@ -54,6 +54,16 @@ for s in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
         python bench.py --no-cpu-baseline --no-parity > gpurun_out/prof_${TAG}.log 2>&1 || { tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
       tail -1 gpurun_out/prof_${TAG}.log ;;
+    mbo)     # micro-batch stream overlap probe (tools/mb_overlap.py)
+      timeout -k 10 200 python -u tools/mb_overlap.py dec 2 > gpurun_out/mbo_${TAG}.txt 2>&1 &&
+      timeout -k 10 200 python -u tools/mb_overlap.py enc 2 >> gpurun_out/mbo_${TAG}.txt 2>&1 || { tail -30 gpurun_out/mbo_${TAG}.txt; exit 1; }
+      cat gpurun_out/mbo_${TAG}.txt ;;
+    abnt)    # same-box whole-step A/B: pending non-temporal LN / attention stores
+      timeout -k 10 600 bash tools/ab_bench.sh mae_clip_amd/libmaeclip.so mae_clip_amd/libmaeclip_nt.so 3 > gpurun_out/abnt_${TAG}.txt 2>&1 || { tail -30 gpurun_out/abnt_${TAG}.txt; exit 1; }
+      cat gpurun_out/abnt_${TAG}.txt ;;
+    sq)      # main-loop rate at large square shapes vs hipBLASLt
+      GEMM_SET=sq timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/sq_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/sq_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/sq_${TAG}.jsonl ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac

@@ -4,7 +4,7 @@
 # command ran (any other status): that result is final.
 # usage: bash tools/gpu_retry.sh OUTFILE 'command'
 out=$1; shift
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${RETRIES:-20}); do
   (cd /root/repo && timeout 1700 /usr/local/graft/bin/gpurun --timeout 1200 -- "$@") > "$out" 2>&1
   rc=$?
   if grep -q "status=transient\|no free box\|slot(s) on this pod are busy\|backing off" "$out" && ! grep -q "status=ok" "$out"; then
