@@ -76,4 +76,5 @@ side_stream = True         # frozen text tower || image encoder; weight-gradient
 dp_encoder_chunk = (1, 2, 3, 6)
 dp_decoder_chunk = 4       # data parallel: decoder blocks per autograd Function (overlapped by the encoder backward)
 dp_grad_dtype = "fp32"     # data parallel gradient all-reduce: "fp32" (exact) or "bf16" (opt-in, half the bytes)
+stack_microbatches = 2     # bf16 stacks: samples cut into this many micro-batches, each chain on its own stream
 wgrad_grouped = True       # all weight gradients of a stack in one grouped GEMM launch (maeclip_wgrad_grouped)

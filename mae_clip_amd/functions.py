@@ -172,6 +172,64 @@ def _q8(f8, M, D, fmt, dev):
 PER_BLOCK = 12  # n1w n1b qkvw qkvb projw projb n2w n2b fc1w fc1b fc2w fc2b
 
 
+_MB_STREAMS = {}
+
+
+def mb_stream(device, i):
+    """Extra HIP stream i (>= 1) per device for micro-batch i of a stack."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, i)
+    s = _MB_STREAMS.get(key)
+    if s is None:
+        s = _MB_STREAMS[key] = torch.cuda.Stream(device=idx)
+    return s
+
+
+class MicroBatches:
+    """The stack's samples cut into S equal micro-batches, each issued on its
+    own stream (micro-batch 0 on the current one). A kernel of one
+    micro-batch fills the CUs the other's kernel leaves idle in its partial
+    last round of tiles and around its launch, so the two chains overlap;
+    every kernel still sees whole samples (attention) and whole 64-row groups
+    (GEMM column-sum partials), so each micro-batch computes exactly the rows
+    the whole-batch launch would (tools/mb_overlap.py: bitwise equal).
+    Outputs are row slices of whole-batch buffers, so the grouped weight
+    gradients and the column reductions run once on the whole batch."""
+
+    def __init__(self, B, n, S, device):
+        self.S = S
+        self.Bs = B // S
+        self.rows = [(i * self.Bs * n, (i + 1) * self.Bs * n) for i in range(S)]
+        self.main = torch.cuda.current_stream(device)
+        self.streams = [self.main] + [mb_stream(device, i) for i in range(1, S)]
+
+    def fork(self):
+        for st in self.streams[1:]:
+            st.wait_stream(self.main)
+
+    def join(self):
+        for st in self.streams[1:]:
+            self.main.wait_stream(st)
+
+    def each(self):
+        """(index, row slice, batch slice) under each micro-batch's stream."""
+        for i, st in enumerate(self.streams):
+            r0, r1 = self.rows[i]
+            with torch.cuda.stream(st):
+                yield i, slice(r0, r1), slice(i * self.Bs, (i + 1) * self.Bs)
+
+
+def microbatch_count(spec) -> int:
+    """Micro-batches for a stack: CFG.stack_microbatches on the bf16 path
+    (fp8 and fp32 parity mode run one), when every micro-batch keeps whole
+    64-row groups of the GEMM column-sum partials."""
+    from . import config as CFG
+    S = int(getattr(CFG, "stack_microbatches", 1) or 1)
+    if S <= 1 or spec.dtype != torch.bfloat16 or spec.w8 is not None or spec.B % S:
+        return 1
+    return S if (spec.B // S * spec.n) % 64 == 0 else 1
+
+
 class TransformerStackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, spec: StackSpec, *params):
@@ -181,21 +239,25 @@ class TransformerStackFn(torch.autograd.Function):
         T = spec.dtype
         M = B * n
         xi = x.reshape(M, D)
+        dev = x.device
+        S = microbatch_count(spec)
+        if S > 1:
+            return TransformerStackFn._forward_mb(ctx, xi, spec, params, S)
         saved = []
         for i, (wqkv, wproj, w1, w2) in enumerate(spec.wT):
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
             f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
-            q1 = _q8(f8[0], M, D, K.FP8_E4M3, x.device)
+            q1 = _q8(f8[0], M, D, K.FP8_E4M3, dev)
             h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T, q8=q1)
             qkv = _fwd(h1, wqkv, f8[0], xq=q1, bias=bqkv)
             del q1
             o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
             x1 = _fwd(o, wproj, f8[1], bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
-            q2 = _q8(f8[2], M, D, K.FP8_E4M3, x.device)
+            q2 = _q8(f8[2], M, D, K.FP8_E4M3, dev)
             h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T, q8=q2)
             # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
-            dgelu = torch.empty((M, w1.shape[0]), device=x.device, dtype=T)
+            dgelu = torch.empty((M, w1.shape[0]), device=dev, dtype=T)
             a = _fwd(h2, w1, f8[2], xq=q2, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
             del q2
             x2 = _fwd(a, w2, f8[3], bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
@@ -205,10 +267,62 @@ class TransformerStackFn(torch.autograd.Function):
         ctx.spec = spec
         ctx.params = params
         ctx.arena = _arena()
+        ctx.S = 1
         return xi.view(B, n, D)
 
     @staticmethod
+    def _forward_mb(ctx, xi, spec, params, S):
+        B, n, D, H = spec.B, spec.n, spec.D, spec.H
+        hd = D // H
+        scale = hd ** -0.5
+        T = spec.dtype
+        M = B * n
+        dev = xi.device
+        mb = MicroBatches(B, n, S, dev)
+        e = lambda shape, dt=T: torch.empty(shape, device=dev, dtype=dt)
+        saved = []
+        # whole-batch buffers allocated on the current stream before the fork;
+        # each micro-batch writes its rows on its own stream
+        for wqkv, wproj, w1, w2 in spec.wT:
+            F = w1.shape[0]
+            saved.append([None, e((M, D)), e((M,), torch.float32), e((M,), torch.float32), e((M, 3 * D)),
+                          e((M, D)), e((B, H, n), torch.float32), e((M, D), torch.float32), e((M, D)),
+                          e((M,), torch.float32), e((M,), torch.float32), e((M, F)), e((M, F))])
+        outs = [e((M, D), torch.float32) for _ in spec.wT]
+        mb.fork()
+        xin = [xi[slice(r0, r1)] for r0, r1 in mb.rows]
+        # block by block, each micro-batch's launches on its stream in turn (the
+        # captured graph then holds S interleaved chains the replay overlaps)
+        for i, (wqkv, wproj, w1, w2) in enumerate(spec.wT):
+            p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
+            n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
+            _, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = saved[i]
+            for mi, rs, bs in mb.each():
+                xr = xin[mi]
+                K.ln_fwd(xr, n1w, n1b, spec.eps, out_dtype=T, y_out=h1[rs], mean_out=m1[rs], rstd_out=r1[rs])
+                K.linear_fwd(h1[rs], wqkv, bias=bqkv, out=qkv[rs])
+                K.attn_fwd(qkv[rs], mb.Bs, n, H, hd, scale, o_out=o[rs], lse_out=lse[bs])
+                K.linear_fwd(o[rs], wproj, bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xr,
+                             out=x1[rs])
+                K.ln_fwd(x1[rs], n2w, n2b, spec.eps, out_dtype=T, y_out=h2[rs], mean_out=m2[rs], rstd_out=r2[rs])
+                K.linear_fwd(h2[rs], w1, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu[rs], out=a[rs])
+                K.linear_fwd(a[rs], w2, bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1[rs],
+                             out=outs[i][rs])
+                xin[mi] = outs[i][rs]
+        mb.join()
+        for i in range(len(spec.wT)):
+            saved[i][0] = xi if i == 0 else outs[i - 1]
+        ctx.saved = saved
+        ctx.spec = spec
+        ctx.params = params
+        ctx.arena = _arena()
+        ctx.S = S
+        return outs[-1].view(B, n, D)
+
+    @staticmethod
     def backward(ctx, gy):
+        if ctx.S > 1:
+            return TransformerStackFn._backward_mb(ctx, gy)
         spec = ctx.spec
         B, n, D, H = spec.B, spec.n, spec.D, spec.H
         hd = D // H
@@ -279,6 +393,91 @@ class TransformerStackFn(torch.autograd.Function):
             del gi
         rb.flush()
         wq.join()
+        ctx.saved = None
+        return (g.view(B, n, D), None, *grads)
+
+    @staticmethod
+    def _backward_mb(ctx, gy):
+        spec = ctx.spec
+        S = ctx.S
+        B, n, D, H = spec.B, spec.n, spec.D, spec.H
+        hd = D // H
+        scale = hd ** -0.5
+        T = spec.dtype
+        M = B * n
+        dev = gy.device
+        params = ctx.params
+        grads = [None] * len(params)
+        rb = K.ReduceBatch()
+        wq = WgradQueue(dev, spec.side, spec.grouped_wgrad)
+        mb = MicroBatches(B, n, S, dev)
+        e = lambda shape, dt=T: torch.empty(shape, device=dev, dtype=dt)
+        f32 = torch.float32
+        Ms = M // S
+        G = K.ln_bwd_partial_rows(Ms)          # LayerNorm partial rows per micro-batch
+        GC = K.gemm_colsum_rows(M)              # GEMM column-sum partial rows (64-row groups)
+        g = gy.reshape(M, D)
+        if not g.is_contiguous():
+            g = g.contiguous()
+        gT = e((M, D))
+        cpart = K.rows_colsum(g, out_bf16=gT)
+        # whole-batch gradient buffers of every block, written per micro-batch
+        bufs = []
+        for wqkv, wproj, w1, w2 in spec.wT:
+            F = w1.shape[0]
+            bufs.append(dict(dA=e((M, F)), dA_part=e((GC, F), f32), dh2=e((M, D)), dx1=e((M, D), f32),
+                             dx1T=e((M, D)), pg2=e((S * G, D), f32), pb2=e((S * G, D), f32),
+                             pc2=e((S * G, D), f32), dO=e((M, D)), dqkv=e((M, 3 * D)), qpart=e((B, 3 * D), f32),
+                             dh1=e((M, D)), dx=e((M, D), f32), dxT=e((M, D)), pg1=e((S * G, D), f32),
+                             pb1=e((S * G, D), f32), pc1=e((S * G, D), f32)))
+        mb.fork()
+        gin = [(g[slice(r0, r1)], gT[slice(r0, r1)]) for r0, r1 in mb.rows]
+        for i in reversed(range(len(spec.wT))):
+            wqkv, wproj, w1, w2 = spec.wT[i]
+            n1w, n2w = params[i * PER_BLOCK], params[i * PER_BLOCK + 6]
+            xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
+            b = bufs[i]
+            for mi, rs, bs in mb.each():
+                gs, gTs = gin[mi]
+                ps = slice(mi * G, (mi + 1) * G)
+                cs = slice(rs.start // 64, rs.stop // 64)
+                K.linear_dgrad(gTs, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu[rs], colsum=b["dA_part"][cs],
+                               out=b["dA"][rs])
+                K.linear_dgrad(b["dA"][rs], w1, out=b["dh2"][rs])
+                K.ln_bwd(b["dh2"][rs], x1[rs], m2[rs], r2[rs], n2w, dres=gs, want_bf16=True, want_colsum=True,
+                         dx_out=b["dx1"][rs], dxb_out=b["dx1T"][rs], pg_out=b["pg2"][ps], pb_out=b["pb2"][ps],
+                         pc_out=b["pc2"][ps])
+                K.linear_dgrad(b["dx1T"][rs], wproj, out=b["dO"][rs])
+                K.attn_bwd(qkv[rs], o[rs], b["dO"][rs], lse[bs], mb.Bs, n, H, hd, scale,
+                           dqkv_out=b["dqkv"][rs], part_out=b["qpart"][bs])
+                K.linear_dgrad(b["dqkv"][rs], wqkv, out=b["dh1"][rs])
+                K.ln_bwd(b["dh1"][rs], xi[rs], m1[rs], r1[rs], n1w, dres=b["dx1"][rs], want_bf16=True,
+                         want_colsum=True, dx_out=b["dx"][rs], dxb_out=b["dxT"][rs], pg_out=b["pg1"][ps],
+                         pb_out=b["pb1"][ps], pc_out=b["pc1"][ps])
+                gin[mi] = (b["dx"][rs], b["dxT"][rs])
+        mb.join()
+        ar = ctx.arena
+        for i in reversed(range(len(spec.wT))):
+            p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
+            xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
+            b = bufs[i]
+            gi = [None] * PER_BLOCK
+            gi[11] = rb.add(cpart, out=gout(ar, p[11]))
+            gi[10] = wq.wgrad(gT, a, out=gout(ar, p[10]))
+            gi[9] = rb.add(b["dA_part"], out=gout(ar, p[9]))
+            gi[8] = wq.wgrad(b["dA"], h2, out=gout(ar, p[8]))
+            gi[6], gi[7] = rb.add(b["pg2"], out=gout(ar, p[6])), rb.add(b["pb2"], out=gout(ar, p[7]))
+            gi[5] = rb.add(b["pc2"], out=gout(ar, p[5]))
+            gi[4] = wq.wgrad(b["dx1T"], o, out=gout(ar, p[4]))
+            gi[3] = rb.add(b["qpart"], out=gout(ar, p[3]))
+            gi[2] = wq.wgrad(b["dqkv"], h1, out=gout(ar, p[2]))
+            gi[0], gi[1] = rb.add(b["pg1"], out=gout(ar, p[0])), rb.add(b["pb1"], out=gout(ar, p[1]))
+            gT, cpart = b["dxT"], b["pc1"]
+            for j in range(PER_BLOCK):
+                grads[i * PER_BLOCK + j] = gi[j].view(p[j].shape)
+        rb.flush()
+        wq.join()
+        g = bufs[0]["dx"]
         ctx.saved = None
         return (g.view(B, n, D), None, *grads)
 

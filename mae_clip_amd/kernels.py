@@ -214,13 +214,14 @@ def gemm_colsum_rows(M: int) -> int:
     return int(L.lib().maeclip_gemm_colsum_rows(M))
 
 
-def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, aux_out=None, colsum=None):
-    """y[M,N] = x[M,K] w[N,K]^T (+bias) with epilogue (nn.Linear forward)."""
+def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, aux_out=None, colsum=None, out=None):
+    """y[M,N] = x[M,K] w[N,K]^T (+bias) with epilogue (nn.Linear forward);
+    out: an [M, N] row-major destination (e.g. a row slice of a larger buffer)."""
     M, K = x.shape
     N = w.shape[0]
     out_dtype = out_dtype or x.dtype
-    y = torch.empty((M, N), device=x.device, dtype=out_dtype)
-    gemm(x, w, y, M, N, K, x.stride(0), w.stride(0), N, KC, KC, epilogue=epilogue, bias=bias, resid=resid,
+    y = out if out is not None else torch.empty((M, N), device=x.device, dtype=out_dtype)
+    gemm(x, w, y, M, N, K, x.stride(0), w.stride(0), y.stride(0), KC, KC, epilogue=epilogue, bias=bias, resid=resid,
          ldr=(resid.stride(0) if resid is not None else 0), aux_out=aux_out,
          ldaux=(aux_out.stride(0) if aux_out is not None else 0), colsum=colsum)
     return y
@@ -349,15 +350,20 @@ def embed_fwd(ids, word, pos, mask=None):
 
 # -------------------------------------------------------------- LayerNorm
 def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dropout=0.0, seed_in=0, seed_out=0,
-           want_stats=True, y2=False, xsum=False, step_ptr=None, q8=None):
+           want_stats=True, y2=False, xsum=False, step_ptr=None, q8=None, y_out=None, mean_out=None, rstd_out=None):
     """Returns (y, mean, rstd, y2_bf16, xsum). q8 (Fp8Rows, optional): also
-    filled with the fp8 row quantisation of y (== quant_rows_fp8(y, q8.fmt))."""
+    filled with the fp8 row quantisation of y (== quant_rows_fp8(y, q8.fmt)).
+    y_out / mean_out / rstd_out: dense destinations (row slices of larger buffers)."""
     _dev(x, gamma, beta, res)
     M, D = x.shape
     dev = x.device
-    y = torch.empty((M, D), device=dev, dtype=out_dtype or x.dtype)
-    mean = torch.empty((M,), device=dev, dtype=torch.float32) if want_stats else None
-    rstd = torch.empty((M,), device=dev, dtype=torch.float32) if want_stats else None
+    y = y_out if y_out is not None else torch.empty((M, D), device=dev, dtype=out_dtype or x.dtype)
+    if y.stride(0) != D:
+        raise ValueError("ln_fwd: y must be dense [M, D] rows")
+    mean = (mean_out if mean_out is not None else torch.empty((M,), device=dev, dtype=torch.float32)) \
+        if want_stats else None
+    rstd = (rstd_out if rstd_out is not None else torch.empty((M,), device=dev, dtype=torch.float32)) \
+        if want_stats else None
     yb = torch.empty((M, D), device=dev, dtype=torch.bfloat16) if y2 else None
     xs = torch.empty((M, D), device=dev, dtype=torch.float32) if xsum else None
     a = L.LnFwdArgs(x=x.data_ptr(), x_dtype=_dt(x), res=_ptr(res), ldres=(res.stride(0) if res is not None else 0),
@@ -376,7 +382,7 @@ def ln_bwd_partial_rows(M: int) -> int:
 
 
 def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False,
-           dres_pool=None, pool_n=0, q8=None):
+           dres_pool=None, pool_n=0, q8=None, dx_out=None, dxb_out=None, pg_out=None, pb_out=None, pc_out=None):
     """Returns (dx f32, dx_bf16, dgamma_partial, dbeta_partial, dx_colsum_partial).
     q8 (Fp8Rows, with want_bf16): also filled with quant_rows_fp8(dx_bf16, q8.fmt).
     dres_pool [M / pool_n, D]: residual gradient = the avg-pool backward of it
@@ -385,11 +391,15 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
     M, D = x.shape
     dev = x.device
     G = ln_bwd_partial_rows(M)
-    dx = torch.empty((M, D), device=dev, dtype=torch.float32)
-    dxb = torch.empty((M, D), device=dev, dtype=torch.bfloat16) if want_bf16 else None
-    pg = torch.empty((G, D), device=dev, dtype=torch.float32) if want_param_grads else None
-    pb = torch.empty((G, D), device=dev, dtype=torch.float32) if want_param_grads else None
-    pc = torch.empty((G, D), device=dev, dtype=torch.float32) if want_colsum else None
+    e = lambda o, shape, dt: o if o is not None else torch.empty(shape, device=dev, dtype=dt)
+    dx = e(dx_out, (M, D), torch.float32)
+    dxb = e(dxb_out, (M, D), torch.bfloat16) if want_bf16 else None
+    pg = e(pg_out, (G, D), torch.float32) if want_param_grads else None
+    pb = e(pb_out, (G, D), torch.float32) if want_param_grads else None
+    pc = e(pc_out, (G, D), torch.float32) if want_colsum else None
+    for t, rows in ((dx, M), (dxb, M), (pg, G), (pb, G), (pc, G)):
+        if t is not None and (t.stride(0) != D or t.shape[0] != rows):
+            raise ValueError("ln_bwd: outputs must be dense rows of the expected count")
     a = L.LnBwdArgs(dy=dy.data_ptr(), dy_dtype=_dt(dy), x=x.data_ptr(), x_dtype=_dt(x), mean=mean.data_ptr(),
                     rstd=rstd.data_ptr(), gamma=gamma.data_ptr(), dres=_ptr(dres), dx=dx.data_ptr(), dx_bf=_ptr(dxb),
                     lddx_bf=D, dgamma_partial=_ptr(pg), dbeta_partial=_ptr(pb), dx_colsum_partial=_ptr(pc),
@@ -402,11 +412,15 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
 
 
 # -------------------------------------------------------------- attention
-def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True, step_ptr=None):
+def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True, step_ptr=None,
+             o_out=None, lse_out=None):
     _dev(qkv, key_mask)
     D = H * hd
-    o = torch.empty((B * n, D), device=qkv.device, dtype=qkv.dtype)
-    lse = torch.empty((B, H, n), device=qkv.device, dtype=torch.float32) if want_lse else None
+    o = o_out if o_out is not None else torch.empty((B * n, D), device=qkv.device, dtype=qkv.dtype)
+    if o.stride(0) != D:
+        raise ValueError("attn_fwd: o must be dense [B*n, D] rows")
+    lse = (lse_out if lse_out is not None else torch.empty((B, H, n), device=qkv.device, dtype=torch.float32)) \
+        if want_lse else None
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=_ptr(lse), dout=None, dqkv=None, key_mask=_ptr(key_mask),
                    colsum_partial=None, ld_qkv=qkv.stride(0), ld_o=D, ld_dqkv=0, B=B, n=n, H=H, head_dim=hd,
                    dtype=_dt(qkv), scale=scale, dropout_p=dropout_p, seed=int(seed), step_ptr=_ptr(step_ptr))
@@ -414,11 +428,14 @@ def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want
     return o, lse
 
 
-def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=None):
+def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=None, dqkv_out=None, part_out=None):
     _dev(qkv, o, dout, lse, key_mask)
     D = H * hd
-    dqkv = torch.empty((B * n, 3 * D), device=qkv.device, dtype=qkv.dtype)
-    part = torch.empty((B, 3 * D), device=qkv.device, dtype=torch.float32) if want_colsum else None
+    dqkv = dqkv_out if dqkv_out is not None else torch.empty((B * n, 3 * D), device=qkv.device, dtype=qkv.dtype)
+    if dqkv.stride(0) != 3 * D:
+        raise ValueError("attn_bwd: dqkv must be dense [B*n, 3D] rows")
+    part = (part_out if part_out is not None else torch.empty((B, 3 * D), device=qkv.device, dtype=torch.float32)) \
+        if want_colsum else None
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(), dout=dout.data_ptr(), dqkv=dqkv.data_ptr(),
                    key_mask=_ptr(key_mask), colsum_partial=_ptr(part), ld_qkv=qkv.stride(0), ld_o=o.stride(0),
                    ld_dqkv=3 * D, B=B, n=n, H=H, head_dim=hd, dtype=_dt(qkv), scale=scale, dropout_p=0.0, seed=0)

@@ -590,3 +590,42 @@ def test_uint8_pixel_batch_equals_normalised_batch(dev, precision, mask_ratio):
     assert torch.equal(out[0][0], out[1][0])
     for n, gr in out[0][1].items():
         assert torch.equal(gr, out[1][1][n]), n
+
+
+def test_stack_microbatches_match_whole_batch(dev):
+    """config.stack_microbatches = 2 (the bf16 stacks' samples split into two
+    chains on two streams, functions.MicroBatches) == one chain: identical
+    loss and bitwise-identical weight gradients (every GEMM / LayerNorm /
+    attention row is computed the same way; the weight gradients run once on
+    the whole-batch buffers); bias and LayerNorm parameter gradients, whose
+    column partials are summed in another grouping, within 1e-5 relative L2.
+    C2 model shapes at B = 128, so both micro-batches keep whole 64-row
+    groups (encoder 64 x 50 rows, decoder 64 x 197)."""
+    from tests.helpers import product_config
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd import functions as Fn
+    kw = dict(VITB_C2)
+    res = {}
+    batch = {k: v.to(dev) for k, v in make_batch(128, 224, seed=5).items()}
+    for S in (1, 2):
+        with product_config(precision="bf16", stack_microbatches=S, **kw):
+            torch.manual_seed(0)
+            m = CLIPModel().to(dev).eval()
+            spec_s = Fn.microbatch_count(Fn.StackSpec(B=128, n=50, D=768, H=12, eps=1e-6, dtype=torch.bfloat16, wT=[]))
+            assert spec_s == S
+            loss = m(batch)
+            loss.backward()
+            torch.cuda.synchronize()
+            res[S] = (loss.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+    (l1, g1), (l2, g2) = res[1], res[2]
+    assert l1 == l2, (l1, l2)
+    worst = 0.0
+    for n, a in g1.items():
+        b = g2[n]
+        if a.dim() >= 2 and "pos_embed" not in n and "token" not in n:
+            assert torch.equal(a, b), n
+        else:
+            e = ((a - b).norm() / (a.norm() + 1e-30)).item()
+            worst = max(worst, e)
+            assert e < 1e-5, (n, e)
+    record_parity("stack_microbatches_2_vs_1", worst_bias_ln_grad_relL2=worst)

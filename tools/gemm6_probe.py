@@ -1,0 +1,80 @@
+"""GEMM v6 (4-wave 128x128-per-wave tiles, csrc/gemm6.hip) against v4 on the
+same inputs: bitwise equality of C and the time of each, for large square and
+production shapes, plain (bf16 out) and RESID (fp32 out) epilogues.
+usage: python tools/gemm6_probe.py          (spawns itself with MAECLIP_GEMM_V6=0/1)"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+SHAPES = [  # name, M, N, K, b_layout, epi(0 plain bf16 / 2 RESID f32)
+    ("sq4096", 4096, 4096, 4096, 0, 0), ("sq8192", 8192, 8192, 8192, 0, 0), ("sq4096 RC", 4096, 4096, 4096, 1, 0),
+    ("enc fc1 fwd", 12800, 3072, 768, 0, 0), ("enc qkv fwd", 12800, 2304, 768, 0, 0),
+    ("enc fc2 fwd+res", 12800, 768, 3072, 0, 2), ("enc fc1 dgrad", 12800, 768, 3072, 1, 0),
+    ("enc qkv dgrad", 12800, 768, 2304, 1, 0), ("dec fc2 fwd+res", 50432, 512, 2048, 0, 2),
+    ("dec fc1 dgrad", 50432, 512, 2048, 1, 0), ("dec qkv dgrad", 50432, 512, 1536, 1, 0),
+    ("dec qkv fwd", 50432, 1536, 512, 0, 0), ("dec proj fwd+res", 50432, 512, 512, 0, 2),
+    ("ragged M", 5000, 768, 1024, 0, 0), ("ragged M res", 777, 512, 640, 1, 2),
+]
+
+
+def child():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    from mae_clip_amd import kernels as K
+    dev = torch.device("cuda")
+    out = {}
+    for name, M, N, Kd, lb, epi in SHAPES:
+        g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + Kd)
+        A = (torch.randn(M, Kd, generator=g) * 0.5).to(dev, torch.bfloat16)
+        B = (torch.randn(N, Kd, generator=g) * 0.5).to(dev, torch.bfloat16) if lb == 0 else \
+            (torch.randn(Kd, N, generator=g) * 0.5).to(dev, torch.bfloat16)
+        bias = torch.randn(N, generator=g).to(dev)
+        if epi == 2:
+            res = torch.randn(M, N, generator=g).to(dev)
+            C = torch.empty(M, N, device=dev, dtype=torch.float32)
+            kw = dict(epilogue=2, resid=res, ldr=N, bias=bias)
+        else:
+            C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            kw = dict(bias=bias)
+        f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, 0, lb, **kw)
+        f()
+        torch.cuda.synchronize()
+        h = hashlib.sha1(C.cpu().view(torch.uint8).numpy().tobytes()).hexdigest()[:16]
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        s.record()
+        for _ in range(reps):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / reps * 1e3
+        out[name] = dict(hash=h, us=round(us, 1), tflops=round(2.0 * M * N * Kd / us / 1e6, 1))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        child()
+        sys.exit(0)
+    res = {}
+    for v in ("0", "1"):
+        env = dict(os.environ, MAECLIP_GEMM_V6=v)
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "child"], env=env, capture_output=True, text=True,
+                           timeout=240)
+        if r.returncode != 0:
+            print(r.stdout[-2000:], r.stderr[-4000:])
+            sys.exit(r.returncode)
+        res[v] = json.loads(r.stdout.strip().splitlines()[-1])
+    bad = 0
+    for name, *_ in SHAPES:
+        a, b = res["0"][name], res["1"][name]
+        eq = a["hash"] == b["hash"]
+        bad += not eq
+        print(json.dumps(dict(name=name, v4_us=a["us"], v6_us=b["us"], v4_tflops=a["tflops"], v6_tflops=b["tflops"],
+                              speedup=round(a["us"] / b["us"], 3), bitwise_equal=eq)))
+    sys.exit(1 if bad else 0)

@@ -64,6 +64,12 @@ for s in $STEPS; do
     sq)      # main-loop rate at large square shapes vs hipBLASLt
       GEMM_SET=sq timeout -k 10 300 python -u tools/gemm_bench.py > gpurun_out/sq_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/sq_${TAG}.jsonl; exit 1; }
       cat gpurun_out/sq_${TAG}.jsonl ;;
+    layout)  # KC x KC vs KC x RC, padded leading dimensions (tools/gemm_layout_probe.py)
+      timeout -k 10 300 python -u tools/gemm_layout_probe.py > gpurun_out/layout_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/layout_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/layout_${TAG}.jsonl ;;
+    v6)      # GEMM v6 vs v4: bitwise equality + time (tools/gemm6_probe.py)
+      timeout -k 10 500 python -u tools/gemm6_probe.py > gpurun_out/v6_${TAG}.jsonl 2>&1 || { tail -40 gpurun_out/v6_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/v6_${TAG}.jsonl ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
