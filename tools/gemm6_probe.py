@@ -8,14 +8,17 @@ import os
 import subprocess
 import sys
 
-SHAPES = [  # name, M, N, K, b_layout, epi(0 plain bf16 / 2 RESID f32)
-    ("sq4096", 4096, 4096, 4096, 0, 0), ("sq8192", 8192, 8192, 8192, 0, 0), ("sq4096 RC", 4096, 4096, 4096, 1, 0),
-    ("enc fc1 fwd", 12800, 3072, 768, 0, 0), ("enc qkv fwd", 12800, 2304, 768, 0, 0),
-    ("enc fc2 fwd+res", 12800, 768, 3072, 0, 2), ("enc fc1 dgrad", 12800, 768, 3072, 1, 0),
-    ("enc qkv dgrad", 12800, 768, 2304, 1, 0), ("dec fc2 fwd+res", 50432, 512, 2048, 0, 2),
-    ("dec fc1 dgrad", 50432, 512, 2048, 1, 0), ("dec qkv dgrad", 50432, 512, 1536, 1, 0),
-    ("dec qkv fwd", 50432, 1536, 512, 0, 0), ("dec proj fwd+res", 50432, 512, 512, 0, 2),
-    ("ragged M", 5000, 768, 1024, 0, 0), ("ragged M res", 777, 512, 640, 1, 2),
+SHAPES = [  # name, M, N, K, b_layout, epi (0 plain bf16 / 2 RESID f32 / 4 GELU_D / 5 MUL_AUX+colsum)
+    # the C2 step's shapes per micro-batch (128 images: encoder 6400 rows, decoder 25216)
+    ("enc qkv fwd", 6400, 2304, 768, 0, 0), ("enc proj fwd+res", 6400, 768, 768, 0, 2),
+    ("enc fc1 fwd gelu'", 6400, 3072, 768, 0, 4), ("enc fc2 fwd+res", 6400, 768, 3072, 0, 2),
+    ("dec qkv fwd", 25216, 1536, 512, 0, 0), ("dec proj fwd+res", 25216, 512, 512, 0, 2),
+    ("dec fc1 fwd gelu'", 25216, 2048, 512, 0, 4), ("dec fc2 fwd+res", 25216, 512, 2048, 0, 2),
+    ("enc fc2 dgrad*gelu'", 6400, 3072, 768, 1, 5), ("enc fc1 dgrad", 6400, 768, 3072, 1, 0),
+    ("dec fc2 dgrad*gelu'", 25216, 2048, 512, 1, 5), ("dec fc1 dgrad", 25216, 512, 2048, 1, 0),
+    ("dec qkv dgrad", 25216, 512, 1536, 1, 0), ("dec proj dgrad", 25216, 512, 512, 1, 0),
+    ("sq8192", 8192, 8192, 8192, 0, 0),
+    ("ragged M gelu'", 5000, 768, 1024, 0, 4), ("ragged M res", 777, 512, 640, 1, 2), ("ragged mulaux", 1000, 1024, 256, 1, 5),
 ]
 
 
@@ -31,17 +34,32 @@ def child():
         B = (torch.randn(N, Kd, generator=g) * 0.5).to(dev, torch.bfloat16) if lb == 0 else \
             (torch.randn(Kd, N, generator=g) * 0.5).to(dev, torch.bfloat16)
         bias = torch.randn(N, generator=g).to(dev)
+        extra = []
         if epi == 2:
             res = torch.randn(M, N, generator=g).to(dev)
             C = torch.empty(M, N, device=dev, dtype=torch.float32)
             kw = dict(epilogue=2, resid=res, ldr=N, bias=bias)
+        elif epi == 4:
+            C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ao = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            kw = dict(epilogue=4, aux_out=ao, ldaux=N, bias=bias)
+            extra = [ao]
+        elif epi == 5:
+            C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            aux = torch.rand(M, N, generator=g).to(dev, torch.bfloat16)
+            cs = torch.empty(K.gemm_colsum_rows(M), N, device=dev)
+            kw = dict(epilogue=5, aux=aux, ldaux=N, colsum=cs)
+            extra = [cs]
         else:
             C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             kw = dict(bias=bias)
         f = lambda: K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, 0, lb, **kw)
         f()
         torch.cuda.synchronize()
-        h = hashlib.sha1(C.cpu().view(torch.uint8).numpy().tobytes()).hexdigest()[:16]
+        hh = hashlib.sha1(C.cpu().view(torch.uint8).numpy().tobytes())
+        for t in extra:
+            hh.update(t.cpu().view(torch.uint8).numpy().tobytes())
+        h = hh.hexdigest()[:16]
         for _ in range(3):
             f()
         torch.cuda.synchronize()
