@@ -32,6 +32,8 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
+int gemm_v6(const maeclip_gemm_args& a, hipStream_t s);
+bool gemm_v6_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_small_ok(const maeclip_gemm_args& a);
 int64_t gemm_small_workspace(const maeclip_gemm_args& a);
@@ -428,7 +430,9 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   int rc = 1;
   // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
   // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
-  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
+  if (forced == 0 && maeclip::gemm_v6_ok(*a))
+    rc = maeclip::gemm_v6(*a, s);
+  else if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
     rc = maeclip::gemm_v4(*a, s);
   else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
            (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))

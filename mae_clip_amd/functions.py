@@ -215,8 +215,22 @@ class MicroBatches:
         """(index, row slice, batch slice) under each micro-batch's stream."""
         for i, st in enumerate(self.streams):
             r0, r1 = self.rows[i]
-            with torch.cuda.stream(st):
-                yield i, slice(r0, r1), slice(i * self.Bs, (i + 1) * self.Bs)
+            _MB_ACTIVE[0] = i
+            try:
+                with torch.cuda.stream(st):
+                    yield i, slice(r0, r1), slice(i * self.Bs, (i + 1) * self.Bs)
+            finally:
+                _MB_ACTIVE[0] = None
+
+
+_MB_ACTIVE = [None]
+
+
+def microbatch_active():
+    """Index of the micro-batch whose launches are being issued (None outside
+    MicroBatches.each): its kernels run concurrently with the other chain's
+    (bench.py's launch timer then reports them as overlapped)."""
+    return _MB_ACTIVE[0]
 
 
 def microbatch_count(spec) -> int:

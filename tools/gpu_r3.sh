@@ -70,6 +70,12 @@ for s in $STEPS; do
     v6)      # GEMM v6 vs v4: bitwise equality + time (tools/gemm6_probe.py)
       timeout -k 10 500 python -u tools/gemm6_probe.py > gpurun_out/v6_${TAG}.jsonl 2>&1 || { tail -40 gpurun_out/v6_${TAG}.jsonl; exit 1; }
       cat gpurun_out/v6_${TAG}.jsonl ;;
+    mbscan)  # micro-batch count x hardware queues, same box (tools/mb_scan.sh)
+      timeout -k 10 900 bash tools/mb_scan.sh > gpurun_out/mbscan_${TAG}.txt 2>&1 || { tail -30 gpurun_out/mbscan_${TAG}.txt; exit 1; }
+      cat gpurun_out/mbscan_${TAG}.txt ;;
+    v6split) # v6 main-loop streams timed apart (tools/v6_stream_split.sh)
+      timeout -k 10 900 bash tools/v6_stream_split.sh > gpurun_out/v6split_${TAG}.txt 2>&1 || { tail -30 gpurun_out/v6split_${TAG}.txt; exit 1; }
+      cat gpurun_out/v6split_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
