@@ -32,7 +32,6 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
-int64_t gemm_v4_workspace(const maeclip_gemm_args& a);
 int gemm_v6(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v6_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
@@ -447,16 +446,11 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
 
 // Scratch bytes maeclip_gemm may use for this call when the caller asks for no
-// split-K itself (splitk <= 1): the small-fp32 path's K-slice partials, or the
-// v4 stream-K counters + partial tiles (the counter words must be zero the
-// first time a workspace is used; every call leaves them zero again, so one
-// workspace serves any number of calls -- on ONE stream at a time).
+// split-K itself (splitk <= 1): the small-fp32 path's K-slice partials.
 extern "C" int64_t maeclip_gemm_workspace(const maeclip_gemm_args* a) {
   if (!a || a->splitk > 1) return 0;
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
-  if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small_workspace(*a);
-  if ((forced == 0 || forced == 8) && !maeclip::gemm_v6_ok(*a)) return maeclip::gemm_v4_workspace(*a);
-  return 0;
+  return (forced != 99 && maeclip::gemm_small_ok(*a)) ? maeclip::gemm_small_workspace(*a) : 0;
 }
 
 // Slice count for split-K (the wgrad shapes of the hot path have only 4-36

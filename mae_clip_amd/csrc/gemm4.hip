@@ -492,41 +492,13 @@ struct WgGroup {
   WgProb p[WG_MAX];
 };
 
-// Stream-K for plain launches (maeclip_gemm, one batch, no split-K): tiles
-// [0, Tdp) run whole over the persistent grid (Tdp a multiple of it), the
-// K-tiles of tiles [Tdp, T) are dealt out in contiguous ranges of skw per
-// block position. A piece of a tile cut between blocks is written as an fp32
-// partial to one of its block's two slots (lane-linear image of acc: fragment
-// f of thread t at byte 8192 f + 16 t, so each wave-instruction moves 1 KiB
-// contiguous); gemm4_skfix_kernel then sums each cut tile's pieces in
-// block-position order (fixed summation order) and runs the ordinary
-// epilogue. No counters, no waiting inside the GEMM launch.
-struct SkPlan {
-  int Tdp, skw, NT;
-  float* ws;
-};
-constexpr int SK_SLOT_BYTES = 65536 * 4;   // one 256x256 fp32 partial
-
-__device__ __forceinline__ void sk_publish(float* ws, int slot, const v4f (&acc)[8][4], int tid) {
-  // scalar slot / fragment offsets, one per-lane VGPR offset (a global store
-  // per fragment would hold 32 64-bit addresses)
-  const rsrc_t rs = make_rsrc((const char*)ws, (int64_t)(slot + 1) * SK_SLOT_BYTES);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rs, tid * 16,
-                                             slot * SK_SLOT_BYTES + (i * 4 + j) * 8192, 0);
-}
-
 // F8: 0 = bf16 operands (K-tile 64); 1 / 2 = fp8 operands, A e4m3 / e5m2 and
 // B e4m3 (K-tile 128 = the same 128 bytes per row), per-row A scales sa[M] and
 // per-column B scales sb[N] applied in the epilogue.
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256, bool SKP = false>
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256>
 __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp,
                                            const float* __restrict__ sa = nullptr,
-                                           const float* __restrict__ sb = nullptr,
-                                           const SkPlan* __restrict__ sk = nullptr) {
+                                           const float* __restrict__ sb = nullptr) {
   static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
   static_assert(BM == 256 || (BM == 192 && LA == LAY_KC && !SPLIT && !GRP), "BM 192: KC A, plain launches only");
   using TM = TileM<BM>;
@@ -543,31 +515,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   // units: standard = output tiles (this block's slice is blockIdx.y);
   // grouped = slice-major (slice, tile) pairs, so neighbouring units share operands
   int T, gn = 1, klen = 0;
-  // stream-K remainder (grouped wgrad: slots reduced by wgrad4_sk_reduce_kernel;
-  // plain: finished in-launch by the last arriving piece)
-  int sk_w = 0, sk_Tdp = 0, sk_NT = 1, sk_T = 0;
   if (GRP) {
     T = gp->skw > 0 ? gp->Tdp : gp->T * gp->S;
     klen = ((gp->Mtok + gp->S - 1) / gp->S + KT - 1) / KT * KT;
-    if (gp->skw > 0) {
-      sk_w = gp->skw;
-      sk_Tdp = gp->Tdp;
-      sk_NT = gp->NT;
-      sk_T = gp->T;
-    }
   } else {
     const int gm = ((int)args.M + BM - 1) / BM;
     gn = ((int)args.N + 255) / 256;
     T = gm * gn;
     const int S = SPLIT ? args.splitk : 1;
     klen = (((int)args.K + S - 1) / S + KT - 1) / KT * KT;
-    if (SKP) {
-      sk_w = sk->skw;
-      sk_Tdp = sk->Tdp;
-      sk_NT = sk->NT;
-      sk_T = T;
-      T = sk->Tdp;
-    }
   }
   auto unit = [&](int u) {
     Unit4 w;
@@ -621,20 +577,20 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   // the remainder tiles
   const int ndp = cbeg + li < cend ? (cend - (cbeg + li) + nbx - 1) / nbx : 0;
   int ska = 0, skb = 0, nsk = 0, skp = 0;
-  if (sk_w > 0) {
+  if (GRP && gp->skw > 0) {
     skp = G % 8 == 0 ? x8 * (G / 8) + li : (int)blockIdx.x;   // XCD-contiguous positions
-    const int tot = (sk_T - sk_Tdp) * sk_NT;
-    ska = min(skp * sk_w, tot);
-    skb = min(ska + sk_w, tot);
-    nsk = skb > ska ? (skb - 1) / sk_NT - ska / sk_NT + 1 : 0;
+    const int tot = (gp->T - gp->Tdp) * gp->NT;
+    ska = min(skp * gp->skw, tot);
+    skb = min(ska + gp->skw, tot);
+    nsk = skb > ska ? (skb - 1) / gp->NT - ska / gp->NT + 1 : 0;
   }
   auto job = [&](int j) -> Unit4 {
     if (j < ndp) return unit(cbeg + li + j * nbx);
-    const int s = j - ndp, NT = sk_NT;
+    const int s = j - ndp, NT = gp->NT;
     const int tl = ska / NT + s;
     const int k0 = s == 0 ? ska % NT : 0;
     const int k1 = tl == (skb - 1) / NT ? (skb - 1) % NT + 1 : NT;
-    Unit4 w = unit(sk_Tdp + tl);
+    Unit4 w = unit(gp->Tdp + tl);
     w.kbeg = k0 * KT;
     w.nt = k1 - k0;
     w.slot = (k0 == 0 && k1 == NT) ? -1 : 2 * skp + (s == 0 ? 0 : 1);
@@ -845,8 +801,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       epilogue4_slab(args.workspace + ((int64_t)z * args.splitk + blockIdx.y) * args.M * args.N, (int)args.M,
                      (int)args.N, args.alpha, acc, m0, n0, wm, wn, lane);
     } else {
-      if (SKP && u.slot >= 0) sk_publish(sk->ws, u.slot, acc, tid);
-      else epilogue4<OutT, EPI, F8 != 0>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
+      epilogue4<OutT, EPI, F8 != 0>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
     }
     STAMP(3);
 #ifdef GEMM4_STAMPS
@@ -858,41 +813,6 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 template <int LA, int LB, typename OutT, int EPI, bool SPLIT, int BM = 256>
 __global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
   gemm4_body<LA, LB, OutT, EPI, SPLIT, false, 0, BM>(args, nullptr);
-}
-
-// stream-K launch of a plain GEMM (BM 256)
-template <int LA, int LB, typename OutT, int EPI>
-__global__ void __launch_bounds__(512) gemm4_sk_kernel(const maeclip_gemm_args args, const SkPlan plan) {
-  gemm4_body<LA, LB, OutT, EPI, false, false, 0, 256, true>(args, nullptr, nullptr, nullptr, &plan);
-}
-
-// cut tile blockIdx.x / 8 of a stream-K launch, wave (wm, wn) = blockIdx.x % 8
-// of it (one wave per workgroup): fold the pieces' partial slots in
-// block-position order (0 + x = x: the exact left fold), then the epilogue of
-// the GEMM launch on the wave's 128 x 64 block.
-template <typename OutT, int EPI>
-__global__ void __launch_bounds__(64) gemm4_skfix_kernel(const maeclip_gemm_args args, const SkPlan plan) {
-  __shared__ __attribute__((aligned(16))) char scr[EPI_SCR];
-  const int tl = blockIdx.x >> 3, w = blockIdx.x & 7, lane = threadIdx.x;
-  const int NT = plan.NT, kw = plan.skw;
-  const int pf = tl * NT / kw, pl = (tl * NT + NT - 1) / kw;
-  if (pf == pl) return;   // one block ran the whole tile and finished it
-  const int gn = ((int)args.N + 255) / 256, tile = plan.Tdp + tl;
-  const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
-  v4f acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  for (int p = pf; p <= pl; ++p) {
-    const int slot = 2 * p + ((p * kw) / NT == tl ? 0 : 1);
-    const char* base = (const char*)plan.ws + (int64_t)slot * SK_SLOT_BYTES + (w * 64 + lane) * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] += *(const v4f*)(base + (i * 4 + j) * 8192);
-  }
-  epilogue4<OutT, EPI>(args, acc, 0, m0, n0, w >> 2, w & 3, lane, scr);
 }
 
 // fp8 operands (maeclip_gemm_fp8): KC x KC, per-row / per-column scales
@@ -987,73 +907,13 @@ bool use_bm192(const maeclip_gemm_args& a, int ncu) {
   return r192 < r256 - 1e-9;
 }
 
-// Stream-K plan of a plain launch (one batch, no split-K): Tdp whole tiles
-// data-parallel, the rest dealt out as skw K-tiles per block (0 = run all
-// tiles data-parallel). Cost model in K-tile times per block: a tile's
-// epilogue E (2 for bf16 output, 4 with fp32 output or aux / residual
-// reads), a cut tile's slot write + fold ~2 + 2 per extra piece. Stream-K is taken when it beats the best data-parallel tile (256 or
-// 192 rows) by 10 %. MAECLIP_GEMM_SK=0 turns it off (A/B), =2 forces it
-// wherever a plan exists (tests).
-struct SkChoice {
-  int skw = 0, Tdp = 0;
-  double cost = 0.0;
-};
-SkChoice sk_choose(const maeclip_gemm_args& a, int ncu, double dp_cost) {
-  SkChoice c;
-  const char* e = getenv("MAECLIP_GEMM_SK");   // 0: off, 2: whenever a plan exists (tests)
-  const int mode = (e && *e) ? atoi(e) : 1;
-  if (mode == 0 || a.batch != 1 || a.splitk > 1 || a.workspace == nullptr) return c;
-  const int gn = (int)((a.N + 255) / 256), T = (int)((a.M + 255) / 256) * gn, NT = (int)(a.K / 64);
-  const double E = (a.out_dtype == MAECLIP_F32 || a.aux || a.resid) ? 4.0 : 2.0;
-  double best = mode == 2 ? 1e30 : 0.9 * dp_cost;
-  for (int d = 0; d * ncu < T; ++d) {
-    const int rem = T - d * ncu;
-    const int skw = (int)(((int64_t)rem * NT + ncu - 1) / ncu);
-    if (skw < (mode == 2 ? 1 : 4)) continue;
-    const double pieces = (double)NT / skw + 1.0;
-    const double cost = d * (NT + E) + skw + E * ((rem + ncu - 1) / ncu) + 2.0 + 2.0 * (pieces - 1.0);
-    if (cost < best) {
-      best = cost;
-      c.skw = skw;
-      c.Tdp = d * ncu;
-      c.cost = cost;
-    }
-  }
-  return c;
-}
-double dp_cost(const maeclip_gemm_args& a, int ncu, int bm) {
-  const int64_t gn = (a.N + 255) / 256, tiles = (a.M + bm - 1) / bm * gn;
-  const double E = (a.out_dtype == MAECLIP_F32 || a.aux || a.resid) ? 4.0 : 2.0;
-  return (bm == 192 ? 0.89 : 1.0) * (double)((tiles + ncu - 1) / ncu) * ((double)(a.K / 64) + E);
-}
-// workspace of a stream-K launch: 2 partial slots per block
-int64_t sk_workspace_bytes(int ncu) { return (int64_t)2 * ncu * SK_SLOT_BYTES; }
-
 template <int LA, int LB, typename OutT, int EPI>
 int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   const int gn = (int)((a.N + 255) / 256);
   const int S = a.splitk > 1 ? a.splitk : 1;
   const int ncu = gemm4_ncu();
   if constexpr (LA == LAY_KC) {
-    const bool bm192 = use_bm192(a, ncu);
-    // stream-K (KC A operand: the forward and input-gradient GEMMs)
-    const SkChoice c = sk_choose(a, ncu, dp_cost(a, ncu, bm192 ? 192 : 256));
-    if (c.skw > 0) {
-      SkPlan plan = {};
-      plan.Tdp = c.Tdp;
-      plan.skw = c.skw;
-      plan.NT = (int)(a.K / 64);
-      plan.ws = a.workspace;
-      auto kern = gemm4_sk_kernel<LA, LB, OutT, EPI>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
-      hipLaunchKernelGGL(kern, dim3(ncu), dim3(512), TileM<256>::LDS_ALL, s, a, plan);
-      MC_CHECK_LAUNCH("maeclip_gemm(v4, stream-K)");
-      const int cut = (int)((a.M + 255) / 256) * gn - c.Tdp;
-      hipLaunchKernelGGL((gemm4_skfix_kernel<OutT, EPI>), dim3(cut * 8), dim3(64), 0, s, a, plan);
-      MC_CHECK_LAUNCH("maeclip_gemm(v4, stream-K fixup)");
-      return 0;
-    }
-    if (bm192) {
+    if (use_bm192(a, ncu)) {
       auto kern = gemm4_kernel<LA, LB, OutT, EPI, false, 192>;
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_ALL);
       const int tiles = (int)((a.M + 191) / 192) * gn;
@@ -1118,16 +978,6 @@ bool gemm_v4_ok(const maeclip_gemm_args& a) {
   if (a.resid && (!al16(a.resid) || a.ldr % 4)) return false;
   if (a.bias && !al16(a.bias)) return false;
   return true;
-}
-
-// scratch a v4 launch of these args can use for stream-K (0: none)
-int64_t gemm_v4_workspace(const maeclip_gemm_args& a) {
-  if (!gemm_v4_ok(a) || a.batch != 1 || a.splitk > 1 || a.a_layout != LAY_KC) return 0;
-  const int ncu = gemm4_ncu();
-  maeclip_gemm_args t = a;
-  t.workspace = (float*)&t;   // any non-null pointer: the plan only asks "is there one"
-  const bool bm192 = a.a_layout == LAY_KC && use_bm192(a, ncu);
-  return sk_choose(t, ncu, dp_cost(a, ncu, bm192 ? 192 : 256)).skw > 0 ? sk_workspace_bytes(ncu) : 0;
 }
 
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {

@@ -771,48 +771,3 @@ def test_combined_loss_backward_matches_torch(dev):
     _, dI, dT = K.clip_loss(I.detach(), T.detach(), 1.0)
     assert torch.allclose(I.grad, 3.0 * dI, rtol=1e-6, atol=1e-9)
     assert torch.allclose(T.grad, 3.0 * dT, rtol=1e-6, atol=1e-9)
-
-
-@pytest.mark.parametrize("mnk", [(1000, 520, 2048), (6400, 768, 3072), (2048, 1536, 512), (300, 264, 1024)])
-def test_gemm_stream_k(dev, mnk, monkeypatch):
-    """Stream-K launches of the v4 kernel (MAECLIP_GEMM_SK=2 forces a plan
-    wherever one exists): cut tiles' fp32 partials folded in block-position
-    order by the fix-up launch, then the same epilogue as a data-parallel
-    launch. Every epilogue against the data-parallel launch (=0) and fp64;
-    stream-K runs twice to check run-to-run bit equality."""
-    M, N, Kd = mnk
-    x = _rand((M, Kd), torch.bfloat16, dev, seed=3)
-    w = _rand((N, Kd), torch.bfloat16, dev, scale=0.05, seed=4)
-    bias = _rand((N,), torch.float32, dev, seed=5)
-    resid = _rand((M, N), torch.float32, dev, seed=6)
-    dy = _rand((M, N), torch.bfloat16, dev, seed=7)
-    aux = _rand((M, Kd), torch.bfloat16, dev, seed=8)
-    ref = _ref_mm(x, w.t()) + bias.double()
-
-    def run(mode):
-        monkeypatch.setenv("MAECLIP_GEMM_SK", mode)
-        out = {}
-        pre = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        out["gelu"] = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU, aux_out=pre)
-        out["pre"] = pre
-        out["resid"] = K.linear_fwd(x, w, bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=resid)
-        part = torch.empty((K.gemm_colsum_rows(M), N), device=dev, dtype=torch.float32)
-        out["plain"] = K.linear_fwd(x, w, bias, out_dtype=torch.float32, colsum=part)
-        out["colsum"] = part
-        out["dgelu"] = K.linear_dgrad(dy, w, epilogue=K.EPI_DGELU, aux=aux, out_dtype=torch.float32)
-        out["mulaux"] = K.linear_dgrad(dy, w, epilogue=K.EPI_MUL_AUX, aux=aux, out_dtype=torch.bfloat16)
-        d = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        out["gelu_d"] = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU_D, aux_out=d)
-        out["gelu_d_aux"] = d
-        torch.cuda.synchronize()
-        return out
-
-    sk, sk2, dp = run("2"), run("2"), run("0")
-    for k in sk:
-        assert torch.equal(sk[k], sk2[k]), k   # deterministic: fixed fold order
-        tol = 1e-2 * max(1.0, dp[k].abs().max().item())
-        assert (sk[k].double() - dp[k].double()).abs().max().item() < tol, k
-    assert (sk["plain"].double() - ref).abs().max().item() < 2e-3 * ref.abs().max().item()
-    assert (sk["resid"].double() - (ref + resid.double())).abs().max().item() < 2e-3 * ref.abs().max().item() + 1e-3
-    cs = K.colsum_reduce(sk["colsum"])
-    assert (cs.double() - sk["plain"].double().sum(0)).abs().max().item() < 1e-3 * max(1.0, M / 64)

@@ -76,13 +76,6 @@ for s in $STEPS; do
     v6split) # v6 main-loop streams timed apart (tools/v6_stream_split.sh)
       timeout -k 10 900 bash tools/v6_stream_split.sh > gpurun_out/v6split_${TAG}.txt 2>&1 || { tail -30 gpurun_out/v6split_${TAG}.txt; exit 1; }
       cat gpurun_out/v6split_${TAG}.txt ;;
-    skprobe) # stream-K vs data-parallel per production shape (tools/gemm_sk_probe.py)
-      timeout -k 10 400 python -u tools/gemm_sk_probe.py > gpurun_out/skprobe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/skprobe_${TAG}.jsonl; exit 1; }
-      cat gpurun_out/skprobe_${TAG}.jsonl ;;
-    skprof) # kernel-level split of the stream-K probe (GEMM launch vs fix-up launch)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/skprof_${TAG} -o run --output-format csv -- \
-        python tools/gemm_sk_probe.py > gpurun_out/skprof_${TAG}.log 2>&1 || { tail -30 gpurun_out/skprof_${TAG}.log; exit 1; }
-      tail -2 gpurun_out/skprof_${TAG}.log ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
