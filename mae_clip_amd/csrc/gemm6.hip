@@ -165,22 +165,28 @@ __global__ void __launch_bounds__(256) gemm6_kernel(const maeclip_gemm_args args
   const int ntiles = cbeg + li < cend ? (cend - (cbeg + li) + nbx - 1) / nbx : 0;
   if (ntiles == 0) return;
 
-  // per-lane DMA byte offsets (loop invariants): A KC rows 8q.. (q = wave + 4i);
-  // B KC likewise, B RC: image i >> 2, k-rows 4qq.. (qq = 4 (i & 3) + wave)
-  int vA[8], vB[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = 8 * (wave + 4 * i) + (lane >> 3), p = lane & 7;
-    vA[i] = (int)(r * lda * 2) + ((p ^ ((r >> 1) & 7)) << 4);
+  // per-lane DMA byte offsets: A KC rows 8q.. (q = wave + 4i); B KC likewise,
+  // B RC: image i >> 2, k-rows 4qq.. (qq = 4 (i & 3) + wave). The swizzle term
+  // does not depend on i (rows / k-rows of instruction i are those of
+  // instruction 0 shifted by a multiple of 16), so one VGPR per operand plus a
+  // uniform per-instruction offset (V6_OA(i), V6_OB(i): SGPR soffset) cover all 8.
+  int vA0, vB0;
+  {
+    const int r = 8 * wave + (lane >> 3), p = lane & 7;
+    vA0 = (int)(r * lda * 2) + ((p ^ ((r >> 1) & 7)) << 4);
     if constexpr (LB == LAY_KC) {
-      vB[i] = (int)(r * ldb * 2) + ((p ^ ((r >> 1) & 7)) << 4);
+      vB0 = (int)(r * ldb * 2) + ((p ^ ((r >> 1) & 7)) << 4);
     } else {
-      const int img = i >> 2, qq = 4 * (i & 3) + wave;
-      const int kr = 4 * qq + (lane >> 4);
+      const int kr = 4 * wave + (lane >> 4);
       const int c = (lane & 15) ^ (swz_rc6(kr) >> 1);
-      vB[i] = (int)(kr * ldb * 2) + (128 * img + 8 * c) * 2;
+      vB0 = (int)(kr * ldb * 2) + 8 * c * 2;
     }
   }
+  // (plain expressions: a lambda call inside these builtins' arguments made the
+  // host pass drop the kernel stubs without a diagnostic, ROCm 7.2)
+  const int sA = (int)(64 * lda), sB = LB == LAY_KC ? (int)(64 * ldb) : (int)(32 * ldb);
+#define V6_OA(i) ((i) * sA)
+#define V6_OB(i) (LB == LAY_KC ? (i) * sB : ((i) & 3) * sB + ((i) >> 2) * 256)
   auto dma = [&](const Tile6& tl, int t, int st) {
     char* sa = smem + st * STAGE;
     char* sbp = sa + OPB;
@@ -188,27 +194,70 @@ __global__ void __launch_bounds__(256) gemm6_kernel(const maeclip_gemm_args args
     const int k0 = t * 64;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(sa + (wave + 4 * i) * 1024), 16, vA[i], k0 * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(sa + (wave + 4 * i) * 1024), 16, vA0, k0 * 2 + V6_OA(i), 0, 0);
     if constexpr (LB == LAY_KC) {
       const rsrc_t rb = make_rsrc6(Bb + (int64_t)tl.n0 * ldb * 2, ((int64_t)N - tl.n0) * ldb * 2);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(sbp + (wave + 4 * i) * 1024), 16, vB[i], k0 * 2, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(sbp + (wave + 4 * i) * 1024), 16, vB0, k0 * 2 + V6_OB(i), 0, 0);
     } else {
       const rsrc_t rb = make_rsrc6(Bb + (int64_t)tl.n0 * 2, ((int64_t)K * ldb - tl.n0) * 2);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(sbp + (i >> 2) * 16384 + (4 * (i & 3) + wave) * 1024),
-                                                 16, vB[i], (int)(k0 * ldb * 2), 0, 0);
+                                                 16, vB0, (int)(k0 * ldb * 2) + V6_OB(i), 0, 0);
     }
   };
 
+#ifdef V6_REG
+  // register-staged variant (diagnostic build, -DV6_REG): item g = K-tile
+  // g % nt of the block's tile g / nt goes global -> 64 VGPRs -> ds_write into
+  // stage g & 1, the same lane-linear images the LDS-DMA writes. Items past the
+  // block's last tile read zeros through an empty descriptor.
+  v4u rA[8], rB[8];
+  auto gload = [&](int g) {
+    const int uu = g / nt, t = g - uu * nt;
+    const Tile6 tl = tile(uu);
+    const bool live = uu < ntiles;
+    const rsrc_t ra = make_rsrc6(Ab + (int64_t)tl.m0 * lda * 2, live ? ((int64_t)M - tl.m0) * lda * 2 : 0);
+    const int k0 = t * 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rA[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, vA0, k0 * 2 + V6_OA(i), 0);
+    if constexpr (LB == LAY_KC) {
+      const rsrc_t rb = make_rsrc6(Bb + (int64_t)tl.n0 * ldb * 2, live ? ((int64_t)N - tl.n0) * ldb * 2 : 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rB[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, vB0, k0 * 2 + V6_OB(i), 0);
+    } else {
+      const rsrc_t rb = make_rsrc6(Bb + (int64_t)tl.n0 * 2, live ? ((int64_t)K * ldb - tl.n0) * 2 : 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rB[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, vB0, (int)(k0 * ldb * 2) + V6_OB(i), 0);
+    }
+  };
+  auto swrite = [&](int st) {
+    char* sa = smem + st * STAGE;
+    char* sbp = sa + OPB;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      *(v4u*)(sa + (wave + 4 * i) * 1024 + lane * 16) = rA[i];
+      if constexpr (LB == LAY_KC) *(v4u*)(sbp + (wave + 4 * i) * 1024 + lane * 16) = rB[i];
+      else *(v4u*)(sbp + (i >> 2) * 16384 + (4 * (i & 3) + wave) * 1024 + lane * 16) = rB[i];
+    }
+  };
+#endif
   const int64_t ldc = args.ldc;
   const float alpha = args.alpha;
   int sb = 0;
   Tile6 cur = tile(0);
+#ifdef V6_REG
+  gload(0);
+  swrite(0);
+  gload(1);
+  swrite(1);
+  gload(2);
+#else
   dma(cur, 0, 0);
   dma(cur, 1, 1);
+#endif
   bool stores_pending = false;
 
   for (int u = 0; u < ntiles; ++u) {
@@ -216,8 +265,12 @@ __global__ void __launch_bounds__(256) gemm6_kernel(const maeclip_gemm_args args
     const Tile6 nxt = has_next ? tile(u + 1) : cur;
     // DMA(0) of this tile landed (DMA(1) and the last tile's epilogue may be in flight)
     constexpr int EV = epi_vm<OutT, EPI>();
+#ifdef V6_REG
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     if (stores_pending) wait_vm<cmin(63, 16 + EV)>();
     else wait_vm<16>();
+#endif
     V6_BARRIER();
 
     v4f acc[8][8];
@@ -257,6 +310,12 @@ __global__ void __launch_bounds__(256) gemm6_kernel(const maeclip_gemm_args args
       }
       // ---- M(t)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef V6_REG
+      V6_BARRIER();
+      swrite(st);                      // item g + 2, loaded one K-tile ago
+      __builtin_amdgcn_sched_barrier(0);
+      gload(u * nt + t + 3);
+#else
       if (t + 1 < nt) {
         if (t == 0 && stores_pending) wait_vm<cmin(63, EV)>();   // DMA(1) is older than the last tile's epilogue
         else wait_vm<0>();
@@ -268,6 +327,7 @@ __global__ void __launch_bounds__(256) gemm6_kernel(const maeclip_gemm_args args
         // the next tile's K-tile 0 (at M(nt-2)) / 1 (at M(nt-1)) into the stage just freed
         dma(nxt, t + 2 - nt, st);
       }
+#endif
       // ---- half 2: ks = 1 MFMAs; ks = 0 fragments of t + 1 (read even in the
       // last K-tile: the values are dead, the stage holds the next tile's data)
       const char* sn = smem + (st ^ 1) * STAGE;

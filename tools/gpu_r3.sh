@@ -76,6 +76,9 @@ for s in $STEPS; do
     v6split) # v6 main-loop streams timed apart (tools/v6_stream_split.sh)
       timeout -k 10 900 bash tools/v6_stream_split.sh > gpurun_out/v6split_${TAG}.txt 2>&1 || { tail -30 gpurun_out/v6split_${TAG}.txt; exit 1; }
       cat gpurun_out/v6split_${TAG}.txt ;;
+    v6reg)   # register-staged v6 main loop (-DV6_REG build) vs v4
+      MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_v6reg.so timeout -k 10 500 python -u tools/gemm6_probe.py > gpurun_out/v6reg_${TAG}.jsonl 2>&1 || { tail -40 gpurun_out/v6reg_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/v6reg_${TAG}.jsonl ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
