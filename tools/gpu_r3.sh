@@ -79,6 +79,9 @@ for s in $STEPS; do
     v6reg)   # register-staged v6 main loop (-DV6_REG build) vs v4
       MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_v6reg.so timeout -k 10 500 python -u tools/gemm6_probe.py > gpurun_out/v6reg_${TAG}.jsonl 2>&1 || { tail -40 gpurun_out/v6reg_${TAG}.jsonl; exit 1; }
       cat gpurun_out/v6reg_${TAG}.jsonl ;;
+    pmcstep) # in-step PMC traffic of the bench's dominant launch (tools/pmc_instep.sh)
+      TAG=$TAG timeout -k 10 900 bash tools/pmc_instep.sh "$PMC_KN" "$PMC_GX" "$PMC_KEY" > gpurun_out/pmcstep_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcstep_${TAG}.txt; exit 1; }
+      tail -2 gpurun_out/pmcstep_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
