@@ -80,7 +80,7 @@ for s in $STEPS; do
       MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_v6reg.so timeout -k 10 500 python -u tools/gemm6_probe.py > gpurun_out/v6reg_${TAG}.jsonl 2>&1 || { tail -40 gpurun_out/v6reg_${TAG}.jsonl; exit 1; }
       cat gpurun_out/v6reg_${TAG}.jsonl ;;
     pmcstep) # in-step PMC traffic of the bench's dominant launch (tools/pmc_instep.sh)
-      TAG=$TAG timeout -k 10 900 bash tools/pmc_instep.sh "$PMC_KN" "$PMC_GX" "$PMC_KEY" > gpurun_out/pmcstep_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcstep_${TAG}.txt; exit 1; }
+      TAG=$TAG PICK=$PMC_PICK timeout -k 10 900 bash tools/pmc_instep.sh "$PMC_KN" "$PMC_GX" "$PMC_KEY" > gpurun_out/pmcstep_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcstep_${TAG}.txt; exit 1; }
       tail -2 gpurun_out/pmcstep_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;

@@ -6,7 +6,7 @@
 # share a pass; FETCH_SIZE is doubled on gfx950). The dominant launch is picked
 # by kernel name (unique in the C2 step) and, for instantiations shared by
 # several shapes, by grid size.
-# usage: TAG=name bash tools/pmc_instep.sh 'KERNEL_NAME_SUBSTRING' GRID_X "SHAPE KEY" [bench args...]
+# usage: TAG=name [PICK=I/K] bash tools/pmc_instep.sh 'KERNEL_NAME_SUBSTRING' GRID_X "SHAPE KEY" [bench args...]
 set -o pipefail
 export TMPDIR=/tmp
 TAG="${TAG:-instep}"
@@ -18,4 +18,4 @@ timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o 
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $OUT/$ctr -o run -- python $B > $OUT/$ctr.log 2>&1 || { tail -20 $OUT/$ctr.log; exit 1; }
 done
-python tools/pmc_instep_summary.py $OUT "$KN" "$GX" "$KEY"
+python tools/pmc_instep_summary.py $OUT "$KN" "$GX" "$KEY" "$PICK"
