@@ -237,7 +237,8 @@ class KernelTimer:
         timestamps (stream-ordered after the replay, no host sync), so the
         timed loop's host turnaround between steps carries no D2H read."""
         if self.captured:
-            self.snaps.append(self.ts.clone())
+            from mae_clip_amd import kernels as K
+            self.snaps.append(K.copy_words(self.ts, torch.empty_like(self.ts)))
 
     def harvest(self):
         """After the timed loop: add the captured launches' durations (ms) of
@@ -489,7 +490,7 @@ def main():
     for _ in range(args.steps):
         loss = step()
         timer.snapshot()
-        loss.item()  # main.py:64 syncs every step
+        runner.loss_value()  # main.py:64 reads the loss every step (published by the step, no copy launch)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timer.harvest()

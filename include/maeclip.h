@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 6
+#define MAECLIP_ABI_VERSION 7
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -512,6 +512,15 @@ int32_t maeclip_counter_add_snap(int64_t* counter, int64_t delta, int64_t* snap,
 /* loss combination on device scalars (CLIP.py total loss + MAE term):
  * out[0] = a[0] + w * b[0] */
 int32_t maeclip_scalar_axpy(const float* a, const float* b, float w, float* out, void* stream);
+/* Pinned, device-mapped host memory (hipHostMalloc mapped) for values the host
+ * reads every step without a copy launch: *host_ptr for the CPU, *dev_ptr for
+ * kernels (e.g. maeclip_copy_f32's dst). The reference reads its loss every
+ * step (main.py:64 loss.item()); a kernel inside the captured step writes it
+ * here instead of a device-to-host copy. */
+int32_t maeclip_host_mapped_alloc(int64_t bytes, void** host_ptr, void** dev_ptr);
+int32_t maeclip_host_mapped_free(void* host_ptr);
+/* dst[0..n) = src[0..n) (f32, small n; dst may be device-mapped host memory) */
+int32_t maeclip_copy_f32(const float* src, float* dst, int64_t n, void* stream);
 /* dst_i[k] = w * s[0] * src_i[k] (src_i NULL: w * s[0]) for two dense f32
  * arrays in one launch (n_i = 0: unused); src_i == dst_i allowed. The
  * backward of a loss that scales stored gradients by the incoming grad_output

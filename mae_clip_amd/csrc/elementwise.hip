@@ -496,6 +496,40 @@ extern "C" int32_t maeclip_scalar_axpy(const float* a, const float* b, float w, 
   return 0;
 }
 
+__global__ void __launch_bounds__(NTH) copy_f32_kernel(const float* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTH) dst[i] = src[i];
+}
+
+extern "C" int32_t maeclip_copy_f32(const float* src, float* dst, int64_t n, void* stream) {
+  MC_CHECK_ARG(n >= 0 && (n == 0 || (src && dst)), "maeclip_copy_f32: bad args");
+  if (n == 0) return 0;
+  const int64_t nb = (n + NTH - 1) / NTH;
+  hipLaunchKernelGGL(copy_f32_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(NTH), 0, (hipStream_t)stream, src,
+                     dst, n);
+  MC_CHECK_LAUNCH("maeclip_copy_f32");
+  return 0;
+}
+
+extern "C" int32_t maeclip_host_mapped_alloc(int64_t bytes, void** host_ptr, void** dev_ptr) {
+  MC_CHECK_ARG(bytes > 0 && host_ptr && dev_ptr, "maeclip_host_mapped_alloc: bad args");
+  void* h = nullptr;
+  void* d = nullptr;
+  MC_CHECK_ARG(hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped) == hipSuccess && h,
+               "maeclip_host_mapped_alloc: hipHostMalloc(%lld) failed", (long long)bytes);
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    MC_CHECK_ARG(false, "maeclip_host_mapped_alloc: no device mapping");
+  }
+  *host_ptr = h;
+  *dev_ptr = d;
+  return 0;
+}
+
+extern "C" int32_t maeclip_host_mapped_free(void* host_ptr) {
+  if (host_ptr) (void)hipHostFree(host_ptr);
+  return 0;
+}
+
 extern "C" int32_t maeclip_scale_by_scalar2(const float* src0, float* dst0, int64_t n0, const float* src1, float* dst1,
                                             int64_t n1, const float* s, float w, void* stream) {
   MC_CHECK_ARG(s != nullptr && n0 >= 0 && n1 >= 0 && (n0 == 0 || dst0) && (n1 == 0 || dst1),

@@ -50,6 +50,8 @@ class CapturedStep:
         self.hp_key = None
         self.graph_grads = None
         self.state_key = None
+        self._host = None   # kernels.HostScalars: the loss, published inside the step (loss_value)
+        self._last = None
 
     def _state_key(self):
         """What a replay bakes in besides the batch: every parameter's storage
@@ -73,6 +75,27 @@ class CapturedStep:
         """Optimizer hyper-parameters baked into the captured AdamW launch."""
         return tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in self.opt.param_groups)
 
+    def _publish(self, loss):
+        """write the loss into pinned, device-mapped host memory from inside the
+        step (a kernel of the step itself, captured with it), so that the host's
+        per-step read (main.py:64) needs no device-to-host copy launch"""
+        self._last = loss.detach()
+        if not loss.is_cuda:
+            return
+        if self._host is None:
+            from . import kernels as K
+            self._host = K.HostScalars(1)
+        self._host.publish(loss.detach().reshape(1).float())
+
+    def loss_value(self) -> float:
+        """The last step's loss as a Python float (the reference's loss.item(),
+        main.py:64): waits for the current stream, then reads the value the step
+        published -- no copy kernel."""
+        if self._host is None:
+            return float(self._last.item())
+        torch.cuda.current_stream().synchronize()
+        return self._host.values()[0]
+
     def _eager(self, batch):
         self.opt.zero_grad(set_to_none=True)
         loss = self.model(batch)
@@ -80,6 +103,7 @@ class CapturedStep:
         if self.dp is not None:
             self.dp.sync_gradients()
         self.opt.step()
+        self._publish(loss)
         # detached: a caller holding the loss must not keep this step's autograd
         # graph (and its AccumulateGrad nodes, bound to the eager stream) alive
         # into the capture
@@ -102,6 +126,7 @@ class CapturedStep:
             if self.dp is not None:
                 self.dp.sync_gradients()
             self.opt.step()
+            self._publish(loss)
         # capture recorded the work without running it: undo its host-side counting
         self.model.step = model_step
         self.opt._advance_host_steps(-1)

@@ -613,6 +613,49 @@ def scalar_axpy(a, b, w):
     return out
 
 
+def copy_words(src, dst):
+    """dst <- src, bit for bit, for small contiguous device tensors of equal byte
+    size (4-byte words through maeclip_copy_f32: one launch of ours instead of
+    a runtime blit kernel)"""
+    _dev(src, dst)
+    nb = src.numel() * src.element_size()
+    if nb != dst.numel() * dst.element_size() or nb % 4 or not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("copy_words: contiguous tensors of one byte size, a multiple of 4")
+    _call("maeclip_copy_f32", src.data_ptr(), dst.data_ptr(), nb // 4, _stream())
+    return dst
+
+
+class HostScalars:
+    """n f32 values in pinned, device-mapped host memory (maeclip_host_mapped_alloc):
+    a kernel writes them on the stream (publish), the host reads them after
+    synchronising that stream (values) -- no device-to-host copy launch."""
+
+    def __init__(self, n=1):
+        self.n = int(n)
+        h, d = C.c_void_p(), C.c_void_p()
+        _call("maeclip_host_mapped_alloc", 4 * self.n, C.byref(h), C.byref(d))
+        self.host, self.dev = h.value, d.value
+        self._view = (C.c_float * self.n).from_address(self.host)
+
+    def publish(self, src):
+        """copy the first n values of device f32 tensor `src` here (stream-ordered)"""
+        _dev(src)
+        if src.dtype != torch.float32 or src.numel() < self.n or not src.is_contiguous():
+            raise TypeError("HostScalars.publish: contiguous f32 device tensor with >= n values")
+        _call("maeclip_copy_f32", src.data_ptr(), self.dev, self.n, _stream())
+
+    def values(self):
+        return [float(v) for v in self._view]
+
+    def __del__(self):
+        try:
+            if getattr(self, "host", None):
+                L.lib().maeclip_host_mapped_free(self.host)
+                self.host = None
+        except Exception:
+            pass
+
+
 def scale_by_scalar(s, w=1.0, x=None, y=None, out_x=None, out_y=None):
     """(w * s[0]) * x and (w * s[0]) * y in one launch (s: device f32 scalar;
     x None: the constant 1, then out_x must be given). Returns (out_x, out_y)."""

@@ -329,6 +329,8 @@ def _partial_runs(dev, sizes, runs, product_config, kw, CLIPModel, AdamW, Captur
                     g["lr"] = 5e-4
             batch = {k: v.to(dev) for k, v in make_batch(B, 32, seed=it).items()}
             losses.append(runner.step(batch).item())
+            # the value the step published into mapped host memory (no copy launch)
+            assert runner.loss_value() == losses[-1], (it, runner.loss_value(), losses[-1])
         runs.append((losses, m, runner))
 
 
@@ -354,6 +356,7 @@ def test_captured_step_matches_eager(dev, precision):
         for it in range(5):
             batch = {k: v.to(dev) for k, v in make_batch(8, 32, seed=it).items()}
             losses.append(runner.step(batch).item())
+            assert runner.loss_value() == losses[-1], (it, runner.loss_value(), losses[-1])
         runs.append((losses, m, opt))
     (le, me, oe), (lg, mg, og) = runs
     assert le == lg, (le, lg)
