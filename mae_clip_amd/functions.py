@@ -238,7 +238,10 @@ def microbatch_count(spec) -> int:
     (fp8 and fp32 parity mode run one), when every micro-batch keeps whole
     64-row groups of the GEMM column-sum partials."""
     from . import config as CFG
+    import os
     S = int(getattr(CFG, "stack_microbatches", 1) or 1)
+    # A/B scans only: MAECLIP_MB_D<width> overrides the count for stacks of that width
+    S = int(os.environ.get(f"MAECLIP_MB_D{spec.D}", S))
     if S <= 1 or spec.dtype != torch.bfloat16 or spec.w8 is not None or spec.B % S:
         return 1
     return S if (spec.B // S * spec.n) % 64 == 0 else 1

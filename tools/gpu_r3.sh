@@ -82,6 +82,9 @@ for s in $STEPS; do
     pmcstep) # in-step PMC traffic of the bench's dominant launch (tools/pmc_instep.sh)
       TAG=$TAG PICK=$PMC_PICK timeout -k 10 900 bash tools/pmc_instep.sh "$PMC_KN" "$PMC_GX" "$PMC_KEY" > gpurun_out/pmcstep_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcstep_${TAG}.txt; exit 1; }
       tail -2 gpurun_out/pmcstep_${TAG}.txt ;;
+    mbstack) # micro-batch count per stack width (tools/mb_stack_scan.sh)
+      timeout -k 10 900 bash tools/mb_stack_scan.sh > gpurun_out/mbstack_${TAG}.txt 2>&1 || { tail -30 gpurun_out/mbstack_${TAG}.txt; exit 1; }
+      cat gpurun_out/mbstack_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
