@@ -85,6 +85,14 @@ for s in $STEPS; do
     mbstack) # micro-batch count per stack width (tools/mb_stack_scan.sh)
       timeout -k 10 900 bash tools/mb_stack_scan.sh > gpurun_out/mbstack_${TAG}.txt 2>&1 || { tail -30 gpurun_out/mbstack_${TAG}.txt; exit 1; }
       cat gpurun_out/mbstack_${TAG}.txt ;;
+    attnstamps) # per-phase cycle split of the attention backward (ATTN_STAMPS build)
+      MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_stamps.so timeout -k 10 200 python -u tools/attn_stamps.py 256 197 16 32 > gpurun_out/attnstamps_${TAG}.txt 2>&1 &&
+      MAECLIP_LIB=$PWD/mae_clip_amd/libmaeclip_stamps.so timeout -k 10 200 python -u tools/attn_fwd_stamps.py 256 197 16 32 >> gpurun_out/attnstamps_${TAG}.txt 2>&1 || { tail -30 gpurun_out/attnstamps_${TAG}.txt; exit 1; }
+      cat gpurun_out/attnstamps_${TAG}.txt ;;
+    pmcattn) # SQ counters of the decoder attention forward and backward (tools/pmc_attn.sh)
+      PMCDIR=gpurun_out/pmca_fwd_${TAG} timeout -k 10 500 bash tools/pmc_attn.sh 256 197 16 32 0 > gpurun_out/pmcattn_${TAG}.txt 2>&1 &&
+      PMCDIR=gpurun_out/pmca_bwd_${TAG} timeout -k 10 500 bash tools/pmc_attn.sh 256 197 16 32 1 >> gpurun_out/pmcattn_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcattn_${TAG}.txt; exit 1; }
+      cat gpurun_out/pmcattn_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
