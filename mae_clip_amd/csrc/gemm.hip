@@ -32,6 +32,9 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
+bool gemm_lib_ok(const maeclip_gemm_args& a);
+int gemm_lib(const maeclip_gemm_args& a, hipStream_t s);
+int64_t gemm_lib_workspace(const maeclip_gemm_args& a);
 int gemm_v6(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v6_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
@@ -428,6 +431,11 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   // splitk_reduce (v1's launch() reduces by itself)
   if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small(*a, s);
   int rc = 1;
+  // plain bf16 GEMMs (no epilogue): the vendor library (gemm_lib.hip)
+  if (forced == 0 && maeclip::gemm_lib_ok(*a)) {
+    rc = maeclip::gemm_lib(*a, s);
+    if (rc != 1) return rc;
+  }
   // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA) wherever
   // its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
   if (forced == 0 && maeclip::gemm_v6_ok(*a))
@@ -445,12 +453,21 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
 
+extern "C" int32_t maeclip_gemm_impl(const maeclip_gemm_args* a) {
+  if (!a) return 0;
+  static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
+  if (forced == 99 || maeclip::gemm_small_ok(*a)) return 0;
+  return (forced == 0 && maeclip::gemm_lib_ok(*a)) ? 1 : 0;
+}
+
 // Scratch bytes maeclip_gemm may use for this call when the caller asks for no
-// split-K itself (splitk <= 1): the small-fp32 path's K-slice partials.
+// split-K itself (splitk <= 1): the small-fp32 path's K-slice partials, or the
+// vendor library's workspace for plain bf16 GEMMs (one workspace per stream).
 extern "C" int64_t maeclip_gemm_workspace(const maeclip_gemm_args* a) {
   if (!a || a->splitk > 1) return 0;
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
-  return (forced != 99 && maeclip::gemm_small_ok(*a)) ? maeclip::gemm_small_workspace(*a) : 0;
+  if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small_workspace(*a);
+  return forced == 0 ? maeclip::gemm_lib_workspace(*a) : 0;
 }
 
 // Slice count for split-K (the wgrad shapes of the hot path have only 4-36

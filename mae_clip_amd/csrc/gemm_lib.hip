@@ -1,0 +1,179 @@
+// Library-shaped GEMMs through hipBLASLt, the vendor library -- the "plain
+// library GEMM" case of the MI355X playbook: C = alpha A op(B) [+ bias] with a
+// bf16 C, or the residual form C = alpha A op(B) + bias + R with fp32 R and C
+// (the epilogues hipBLASLt runs itself: its BIAS epilogue, beta = 1 on an fp32
+// C), at K > 512. Everything else -- GELU / GELU' / dGELU / mul-aux epilogues,
+// column-sum partials, K = 512 (the MAE decoder's qkv / fc1 forward, proj
+// dgrad: 0.83-0.98x here), fp8, the grouped weight gradients -- stays on this
+// library's own kernels (gemm4.hip).
+//
+// Why (profiles/r04/plain_gemm_vendor_probe_r4u.jsonl, same box): at K >= 768
+// the vendor's stream-K kernels run 1.00-1.84x of v4 on the step's plain shapes
+// (1.84x: encoder fc1 dgrad at the micro-batch's 6400 rows, one partial round
+// of v4 tiles), at K = 512 0.83-0.98x; the whole C2 step gains 2.1 % with the
+// plain bf16 launches there (plain_gemm_vendor_ab_r4t.txt) and 4.2 % with the
+// residual-form forwards as well (gemm_vendor_modes_ab_r4v.txt: 10032 -> 10456
+// img/s, three rounds each on one box). MAECLIP_GEMM_LIB=0 keeps every GEMM on
+// v4 (A/B, tests of the own kernels).
+//
+// Layout: row-major C[M,N] = A[M,K] op(B) is, column-major, C^T[N,M] =
+// op(B)^T A^T, where A^T is A's storage read column-major ([K,M], ld lda) and
+// op(B)^T is B's storage read column-major: [K,N] transposed (KC B, stored
+// [N][K]) or [N,K] as is (RC B, stored [K][N]).
+#include "common.h"
+#include <hipblaslt/hipblaslt.h>
+#include <stdlib.h>
+#include <mutex>
+#include <unordered_map>
+#include "../../include/maeclip.h"
+
+namespace {
+
+enum { LAY_KC = 0, LAY_RC = 1 };
+constexpr int64_t LIB_WS = 32ll << 20;   // workspace offered to hipBLASLt's heuristic (stream-K partials)
+
+struct LibKey {
+  int64_t M, N, K, lda, ldb, ldc, ldr;
+  int lb, out, ws, bias, res;
+  bool operator==(const LibKey& o) const {
+    return M == o.M && N == o.N && K == o.K && lda == o.lda && ldb == o.ldb && ldc == o.ldc && ldr == o.ldr &&
+           lb == o.lb && out == o.out && ws == o.ws && bias == o.bias && res == o.res;
+  }
+};
+struct LibKeyHash {
+  size_t operator()(const LibKey& k) const {
+    size_t h = 1469598103934665603ull;
+    for (int64_t v : {k.M, k.N, k.K, k.lda, k.ldb, k.ldc, k.ldr, (int64_t)k.lb, (int64_t)k.out, (int64_t)k.ws,
+                      (int64_t)k.bias, (int64_t)k.res})
+      h = (h ^ (size_t)v) * 1099511628211ull;
+    return h;
+  }
+};
+struct LibPlan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr, lr = nullptr;   // lr: the residual C (fp32)
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  bool ok = false;
+};
+
+struct LibState {
+  std::mutex mu;
+  hipblasLtHandle_t handle[64] = {};
+  std::unordered_map<LibKey, LibPlan, LibKeyHash> plans[64];
+};
+LibState& state() {
+  static LibState s;
+  return s;
+}
+
+// MAECLIP_GEMM_LIB: 0 = off (v4 for every plain GEMM), 2 = bf16 outputs only
+int lib_mode() {
+  const char* e = getenv("MAECLIP_GEMM_LIB");
+  return (e && *e) ? atoi(e) : 1;
+}
+
+// plan (descriptors + the heuristic's first algorithm) of one shape, cached per device
+const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  LibState& st = state();
+  std::lock_guard<std::mutex> lock(st.mu);
+  if (!st.handle[dev] && hipblasLtCreate(&st.handle[dev]) != HIPBLAS_STATUS_SUCCESS) {
+    st.handle[dev] = nullptr;
+    return nullptr;
+  }
+  const bool res = a.epilogue == 2;   // EPI_RESID
+  const LibKey key{a.M, a.N, a.K, a.lda, a.ldb, a.ldc, res ? a.ldr : 0, a.b_layout, a.out_dtype, have_ws ? 1 : 0,
+                   a.bias ? 1 : 0, res ? 1 : 0};
+  auto it = st.plans[dev].find(key);
+  if (it != st.plans[dev].end()) return it->second.ok ? &it->second : nullptr;
+  LibPlan& p = st.plans[dev][key];
+  const hipDataType ct = a.out_dtype == MAECLIP_BF16 ? HIP_R_16BF : HIP_R_32F;
+  bool ok = hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS;
+  const hipblasOperation_t ta = a.b_layout == LAY_KC ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
+  ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)) == HIPBLAS_STATUS_SUCCESS;
+  // first operand: op(B)^T, [N x K] after its op; second: A^T [K x M]; C / D: [N x M]
+  if (a.b_layout == LAY_KC) ok = ok && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, a.K, a.N, a.ldb) == HIPBLAS_STATUS_SUCCESS;
+  else ok = ok && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, a.N, a.K, a.ldb) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, a.K, a.M, a.lda) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.lc, ct, a.N, a.M, a.ldc) == HIPBLAS_STATUS_SUCCESS;
+  if (res) ok = ok && hipblasLtMatrixLayoutCreate(&p.lr, HIP_R_32F, a.N, a.M, a.ldr) == HIPBLAS_STATUS_SUCCESS;
+  if (a.bias) {
+    // bias per output column n = per row of the column-major D: hipBLASLt's BIAS epilogue
+    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_32F;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)) == HIPBLAS_STATUS_SUCCESS;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)) ==
+                   HIPBLAS_STATUS_SUCCESS;
+    const void* bp = a.bias;   // a valid pointer for the heuristic; re-set at every call
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)) ==
+                   HIPBLAS_STATUS_SUCCESS;
+  }
+  if (ok) {
+    hipblasLtMatmulPreference_t pref = nullptr;
+    const uint64_t wsb = have_ws ? (uint64_t)LIB_WS : 0;
+    ok = hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
+         hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)) ==
+             HIPBLAS_STATUS_SUCCESS;
+    hipblasLtMatmulHeuristicResult_t hr[1];
+    int n = 0;
+    ok = ok && hipblasLtMatmulAlgoGetHeuristic(st.handle[dev], p.desc, p.la, p.lb, res ? p.lr : p.lc, p.lc, pref, 1, hr,
+                                               &n) == HIPBLAS_STATUS_SUCCESS && n > 0 && hr[0].state == HIPBLAS_STATUS_SUCCESS;
+    if (ok) {
+      p.algo = hr[0].algo;
+      p.ws = hr[0].workspaceSize;
+      ok = p.ws <= (size_t)wsb;
+    }
+    if (pref) hipblasLtMatmulPreferenceDestroy(pref);
+  }
+  p.ok = ok;
+  return ok ? &p : nullptr;
+}
+
+}  // namespace
+
+namespace maeclip {
+
+// GEMMs the vendor path takes: bf16 A (KC) and B, one batch, no split-K, no
+// beta / column sums, K > 512; epilogue none (bf16 C) or the fp32 residual
+// (fp32 R and C), each with or without bias. MAECLIP_GEMM_LIB: 0 = off,
+// 2 = bf16-C launches only, 3 = every K (A/B)
+bool gemm_lib_ok(const maeclip_gemm_args& a) {
+  const int mode = lib_mode();
+  if (mode == 0) return false;
+  if (a.dtype != MAECLIP_BF16 || a.a_layout != LAY_KC || a.colsum_partial || a.aux || a.aux_out) return false;
+  if (a.beta != 0.f || a.batch != 1 || a.splitk > 1) return false;
+  const bool plain = a.epilogue == 0 && !a.resid && a.out_dtype == MAECLIP_BF16;
+  const bool res = a.epilogue == 2 && a.resid && a.out_dtype == MAECLIP_F32 && mode != 2;
+  if (!plain && !res) return false;
+  if (a.K <= 512 && mode != 3) return false;
+  return a.M >= 256 && a.N >= 256;
+}
+
+int64_t gemm_lib_workspace(const maeclip_gemm_args& a) { return gemm_lib_ok(a) ? LIB_WS : 0; }
+
+// 0 = done, 1 = not taken (no plan for the shape: the caller falls back to the
+// library's own kernels)
+int gemm_lib(const maeclip_gemm_args& a, hipStream_t s) {
+  const bool have_ws = a.workspace != nullptr;
+  const LibPlan* p = plan_for(a, have_ws);
+  if (!p) return 1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const bool res = a.epilogue == 2;
+  const float alpha = a.alpha, beta = res ? 1.f : 0.f;
+  if (a.bias) {
+    const void* bp = a.bias;
+    MC_CHECK_ARG(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)) ==
+                     HIPBLAS_STATUS_SUCCESS, "maeclip_gemm: hipBLASLt bias pointer");
+  }
+  const hipblasStatus_t r = hipblasLtMatmul(state().handle[dev], p->desc, &alpha, a.B, p->la, a.A, p->lb, &beta,
+                                            res ? (const void*)a.resid : a.C, res ? p->lr : p->lc, a.C, p->lc, &p->algo,
+                                            have_ws ? (void*)a.workspace : nullptr, p->ws, s);
+  MC_CHECK_ARG(r == HIPBLAS_STATUS_SUCCESS, "maeclip_gemm: hipblasLtMatmul failed (status %d)", (int)r);
+  return 0;
+}
+
+}  // namespace maeclip

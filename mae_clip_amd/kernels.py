@@ -50,6 +50,21 @@ def _call(name, *args):
 
 
 # ------------------------------------------------------------------ GEMM
+_SCRATCH = {}
+
+
+def _stream_scratch(device, nbytes):
+    """Per-(device, stream) scratch kept for the process (the vendor library's
+    workspace of maeclip_gemm's plain GEMMs): launches on one stream run in
+    order and share it; a concurrently running stream gets its own."""
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() * 4 < nbytes:
+        t = torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32)
+        _SCRATCH[key] = t
+    return t
+
+
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=EPI_NONE, alpha=1.0, beta=0.0,
          bias=None, aux=None, aux_out=None, ldaux=0, resid=None, ldr=0, colsum=None, batch=1,
          strides=(0, 0, 0), splitk=1, workspace=None):
@@ -62,10 +77,11 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
                    alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
                    resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum), splitk=splitk,
                    workspace=_ptr(workspace))
-    if workspace is None and A.dtype == torch.float32:
+    if workspace is None and splitk <= 1:
         nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
         if nb > 0:
-            workspace = torch.empty((nb // 4,), device=A.device, dtype=torch.float32)
+            workspace = (torch.empty((nb // 4,), device=A.device, dtype=torch.float32) if A.dtype == torch.float32
+                         else _stream_scratch(A.device, nb))
             a.workspace = workspace.data_ptr()
     if LAUNCH_HOOK is None:
         _call("maeclip_gemm", C.byref(a), _stream())
@@ -82,6 +98,8 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
             nbytes += M * N * 4 * batch
         key = (f"M{M} N{N} K{K} {'KR'[a_layout]}{'KR'[b_layout]} epi{epilogue} "
                f"{'bf16' if A.dtype == torch.bfloat16 else 'f32'}>{'bf16' if Cout.dtype == torch.bfloat16 else 'f32'}")
+        if int(L.lib().maeclip_gemm_impl(C.byref(a))) == 1:
+            key += " [hipBLASLt]"   # the vendor library runs this launch (gemm_lib.hip)
         LAUNCH_HOOK(key, 2.0 * M * N * K * batch, nbytes, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
 
 

@@ -93,6 +93,12 @@ for s in $STEPS; do
       PMCDIR=gpurun_out/pmca_fwd_${TAG} timeout -k 10 500 bash tools/pmc_attn.sh 256 197 16 32 0 > gpurun_out/pmcattn_${TAG}.txt 2>&1 &&
       PMCDIR=gpurun_out/pmca_bwd_${TAG} timeout -k 10 500 bash tools/pmc_attn.sh 256 197 16 32 1 >> gpurun_out/pmcattn_${TAG}.txt 2>&1 || { tail -30 gpurun_out/pmcattn_${TAG}.txt; exit 1; }
       cat gpurun_out/pmcattn_${TAG}.txt ;;
+    plainlib) # plain bf16 GEMMs on the vendor library, whole-step A/B (tools/plain_lib_ab.sh)
+      timeout -k 10 900 bash tools/plain_lib_ab.sh > gpurun_out/plainlib_${TAG}.txt 2>&1 || { tail -30 gpurun_out/plainlib_${TAG}.txt; exit 1; }
+      cat gpurun_out/plainlib_${TAG}.txt ;;
+    plainprobe) # per-shape own vs vendor plain GEMMs (tools/plain_gemm_probe.py)
+      timeout -k 10 400 python -u tools/plain_gemm_probe.py > gpurun_out/plainprobe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/plainprobe_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/plainprobe_${TAG}.jsonl ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
