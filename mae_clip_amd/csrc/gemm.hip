@@ -33,8 +33,9 @@ int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
 bool gemm_lib_ok(const maeclip_gemm_args& a);
-int gemm_lib(const maeclip_gemm_args& a, hipStream_t s);
+int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a = nullptr, const float* scale_b = nullptr);
 int64_t gemm_lib_workspace(const maeclip_gemm_args& a);
+bool gemm_lib_fp8_ok(const maeclip_gemm_args& a);
 int gemm_v6(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v6_ok(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
@@ -457,7 +458,7 @@ extern "C" int32_t maeclip_gemm_impl(const maeclip_gemm_args* a) {
   if (!a) return 0;
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
   if (forced == 99 || maeclip::gemm_small_ok(*a)) return 0;
-  return (forced == 0 && maeclip::gemm_lib_ok(*a)) ? 1 : 0;
+  return (forced == 0 && (maeclip::gemm_lib_ok(*a) || maeclip::gemm_lib_fp8_ok(*a))) ? 1 : 0;
 }
 
 // Scratch bytes maeclip_gemm may use for this call when the caller asks for no

@@ -989,6 +989,11 @@ int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
 }  // namespace maeclip
 
 // ------------------------------------------------------------ fp8 operands
+namespace maeclip {
+bool gemm_lib_fp8_ok(const maeclip_gemm_args& a);
+int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a, const float* scale_b);
+}  // namespace maeclip
+
 namespace {
 
 template <typename OutT, int EPI, int F8>
@@ -1055,6 +1060,12 @@ extern "C" int32_t maeclip_gemm_fp8(const maeclip_gemm_args* a, const float* sca
   const int64_t lim = 0x7fffffffLL;
   MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "maeclip_gemm_fp8: operand exceeds 2^31 bytes");
   hipStream_t s = (hipStream_t)stream;
+  // no-epilogue / residual-form launches at K > 512: the vendor library with
+  // outer-vector scales (gemm_lib.hip); every other epilogue below
+  if (maeclip::gemm_lib_fp8_ok(*a)) {
+    const int rc = maeclip::gemm_lib(*a, s, scale_a, scale_b);
+    if (rc != 1) return rc;
+  }
   const bool e5 = a->dtype == MAECLIP_FP8_E5M2;
   if (a->out_dtype == MAECLIP_BF16)
     return e5 ? epi_f8<bf16_t, 2>(*a, scale_a, scale_b, s) : epi_f8<bf16_t, 1>(*a, scale_a, scale_b, s);

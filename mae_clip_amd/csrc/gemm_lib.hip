@@ -34,17 +34,17 @@ constexpr int64_t LIB_WS = 32ll << 20;   // workspace offered to hipBLASLt's heu
 
 struct LibKey {
   int64_t M, N, K, lda, ldb, ldc, ldr;
-  int lb, out, ws, bias, res;
+  int lb, out, ws, bias, res, at;
   bool operator==(const LibKey& o) const {
     return M == o.M && N == o.N && K == o.K && lda == o.lda && ldb == o.ldb && ldc == o.ldc && ldr == o.ldr &&
-           lb == o.lb && out == o.out && ws == o.ws && bias == o.bias && res == o.res;
+           lb == o.lb && out == o.out && ws == o.ws && bias == o.bias && res == o.res && at == o.at;
   }
 };
 struct LibKeyHash {
   size_t operator()(const LibKey& k) const {
     size_t h = 1469598103934665603ull;
     for (int64_t v : {k.M, k.N, k.K, k.lda, k.ldb, k.ldc, k.ldr, (int64_t)k.lb, (int64_t)k.out, (int64_t)k.ws,
-                      (int64_t)k.bias, (int64_t)k.res})
+                      (int64_t)k.bias, (int64_t)k.res, (int64_t)k.at})
       h = (h ^ (size_t)v) * 1099511628211ull;
     return h;
   }
@@ -74,7 +74,8 @@ int lib_mode() {
 }
 
 // plan (descriptors + the heuristic's first algorithm) of one shape, cached per device
-const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws) {
+const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws, const float* scale_a = nullptr,
+                        const float* scale_b = nullptr) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   LibState& st = state();
@@ -85,7 +86,7 @@ const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws) {
   }
   const bool res = a.epilogue == 2;   // EPI_RESID
   const LibKey key{a.M, a.N, a.K, a.lda, a.ldb, a.ldc, res ? a.ldr : 0, a.b_layout, a.out_dtype, have_ws ? 1 : 0,
-                   a.bias ? 1 : 0, res ? 1 : 0};
+                   a.bias ? 1 : 0, res ? 1 : 0, a.dtype};
   auto it = st.plans[dev].find(key);
   if (it != st.plans[dev].end()) return it->second.ok ? &it->second : nullptr;
   LibPlan& p = st.plans[dev][key];
@@ -94,10 +95,25 @@ const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws) {
   const hipblasOperation_t ta = a.b_layout == LAY_KC ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = HIPBLAS_OP_N;
   ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)) == HIPBLAS_STATUS_SUCCESS;
   ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)) == HIPBLAS_STATUS_SUCCESS;
-  // first operand: op(B)^T, [N x K] after its op; second: A^T [K x M]; C / D: [N x M]
-  if (a.b_layout == LAY_KC) ok = ok && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, a.K, a.N, a.ldb) == HIPBLAS_STATUS_SUCCESS;
-  else ok = ok && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, a.N, a.K, a.ldb) == HIPBLAS_STATUS_SUCCESS;
-  ok = ok && hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, a.K, a.M, a.lda) == HIPBLAS_STATUS_SUCCESS;
+  // first operand: op(B)^T, [N x K] after its op; second: A^T [K x M]; C / D: [N x M].
+  // fp8 (maeclip_gemm_fp8): A e4m3 / e5m2, B e4m3, per-row A and per-column B
+  // dequantisation scales as hipBLASLt's outer-vector scales (its first operand
+  // is our B: N scales; its second our A: M scales)
+  const bool f8 = a.dtype == MAECLIP_FP8_E4M3 || a.dtype == MAECLIP_FP8_E5M2;
+  const hipDataType tB = f8 ? HIP_R_8F_E4M3 : HIP_R_16BF;
+  const hipDataType tA = a.dtype == MAECLIP_FP8_E5M2 ? HIP_R_8F_E5M2 : f8 ? HIP_R_8F_E4M3 : HIP_R_16BF;
+  if (a.b_layout == LAY_KC) ok = ok && hipblasLtMatrixLayoutCreate(&p.la, tB, a.K, a.N, a.ldb) == HIPBLAS_STATUS_SUCCESS;
+  else ok = ok && hipblasLtMatrixLayoutCreate(&p.la, tB, a.N, a.K, a.ldb) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.lb, tA, a.K, a.M, a.lda) == HIPBLAS_STATUS_SUCCESS;
+  if (f8) {
+    const hipblasLtMatmulMatrixScale_t sm = HIPBLASLT_MATMUL_MATRIX_SCALE_OUTER_VEC_32F;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_A_SCALE_MODE, &sm, sizeof(sm)) == HIPBLAS_STATUS_SUCCESS;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_B_SCALE_MODE, &sm, sizeof(sm)) == HIPBLAS_STATUS_SUCCESS;
+    const void* sp = scale_b;   // valid pointers for the heuristic; re-set at every call
+    const void* sq = scale_a;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_A_SCALE_POINTER, &sp, sizeof(sp)) == HIPBLAS_STATUS_SUCCESS;
+    ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &sq, sizeof(sq)) == HIPBLAS_STATUS_SUCCESS;
+  }
   ok = ok && hipblasLtMatrixLayoutCreate(&p.lc, ct, a.N, a.M, a.ldc) == HIPBLAS_STATUS_SUCCESS;
   if (res) ok = ok && hipblasLtMatrixLayoutCreate(&p.lr, HIP_R_32F, a.N, a.M, a.ldr) == HIPBLAS_STATUS_SUCCESS;
   if (a.bias) {
@@ -140,10 +156,10 @@ namespace maeclip {
 // beta / column sums, K > 512; epilogue none (bf16 C) or the fp32 residual
 // (fp32 R and C), each with or without bias. MAECLIP_GEMM_LIB: 0 = off,
 // 2 = bf16-C launches only, 3 = every K (A/B)
-bool gemm_lib_ok(const maeclip_gemm_args& a) {
+bool lib_shape_ok(const maeclip_gemm_args& a) {
   const int mode = lib_mode();
   if (mode == 0) return false;
-  if (a.dtype != MAECLIP_BF16 || a.a_layout != LAY_KC || a.colsum_partial || a.aux || a.aux_out) return false;
+  if (a.a_layout != LAY_KC || a.colsum_partial || a.aux || a.aux_out) return false;
   if (a.beta != 0.f || a.batch != 1 || a.splitk > 1) return false;
   const bool plain = a.epilogue == 0 && !a.resid && a.out_dtype == MAECLIP_BF16;
   const bool res = a.epilogue == 2 && a.resid && a.out_dtype == MAECLIP_F32 && mode != 2;
@@ -152,13 +168,23 @@ bool gemm_lib_ok(const maeclip_gemm_args& a) {
   return a.M >= 256 && a.N >= 256;
 }
 
-int64_t gemm_lib_workspace(const maeclip_gemm_args& a) { return gemm_lib_ok(a) ? LIB_WS : 0; }
+bool gemm_lib_ok(const maeclip_gemm_args& a) { return a.dtype == MAECLIP_BF16 && lib_shape_ok(a); }
+
+// fp8 operands (maeclip_gemm_fp8: KC x KC, B e4m3): the same epilogue forms
+bool gemm_lib_fp8_ok(const maeclip_gemm_args& a) {
+  if (a.dtype != MAECLIP_FP8_E4M3 && a.dtype != MAECLIP_FP8_E5M2) return false;
+  const char* e = getenv("MAECLIP_GEMM_LIB_FP8");   // 0: fp8 GEMMs on the own kernel (A/B)
+  if (e && *e == '0') return false;
+  return a.b_layout == LAY_KC && lib_shape_ok(a);
+}
+
+int64_t gemm_lib_workspace(const maeclip_gemm_args& a) { return (gemm_lib_ok(a) || gemm_lib_fp8_ok(a)) ? LIB_WS : 0; }
 
 // 0 = done, 1 = not taken (no plan for the shape: the caller falls back to the
 // library's own kernels)
-int gemm_lib(const maeclip_gemm_args& a, hipStream_t s) {
+int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a, const float* scale_b) {
   const bool have_ws = a.workspace != nullptr;
-  const LibPlan* p = plan_for(a, have_ws);
+  const LibPlan* p = plan_for(a, have_ws, scale_a, scale_b);
   if (!p) return 1;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -168,6 +194,15 @@ int gemm_lib(const maeclip_gemm_args& a, hipStream_t s) {
     const void* bp = a.bias;
     MC_CHECK_ARG(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)) ==
                      HIPBLAS_STATUS_SUCCESS, "maeclip_gemm: hipBLASLt bias pointer");
+  }
+  if (scale_a) {
+    const void* sp = scale_b;
+    const void* sq = scale_a;
+    MC_CHECK_ARG(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_A_SCALE_POINTER, &sp, sizeof(sp)) ==
+                         HIPBLAS_STATUS_SUCCESS &&
+                     hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &sq, sizeof(sq)) ==
+                         HIPBLAS_STATUS_SUCCESS,
+                 "maeclip_gemm_fp8: hipBLASLt scale pointers");
   }
   const hipblasStatus_t r = hipblasLtMatmul(state().handle[dev], p->desc, &alpha, a.B, p->la, a.A, p->lb, &beta,
                                             res ? (const void*)a.resid : a.C, res ? p->lr : p->lc, a.C, p->lc, &p->algo,

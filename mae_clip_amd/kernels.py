@@ -204,6 +204,9 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
                    ldaux=(aux.stride(0) if aux is not None else aux_out.stride(0) if aux_out is not None else 0),
                    resid=_ptr(resid), ldr=(resid.stride(0) if resid is not None else 0),
                    colsum_partial=_ptr(colsum), splitk=1, workspace=None)
+    nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
+    if nb > 0:   # the vendor library's workspace (gemm_lib.hip)
+        a.workspace = _stream_scratch(A.q.device, nb).data_ptr()
     launch = lambda: _call("maeclip_gemm_fp8", C.byref(a), A.s.data_ptr(), B.s.data_ptr(), _stream())
     if LAUNCH_HOOK is None:
         launch()
@@ -216,6 +219,8 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
     if resid is not None:
         nbytes += M * N * 4
     key = f"M{M} N{N} K{K} KK epi{epilogue} fp8{'e5' if A.fmt == FP8_E5M2 else 'e4'}>{'bf16' if ec == 2 else 'f32'}"
+    if int(L.lib().maeclip_gemm_impl(C.byref(a))) == 1:
+        key += " [hipBLASLt]"
     LAUNCH_HOOK(key, 2.0 * M * N * K, nbytes, launch)
     return Cout
 

@@ -99,6 +99,15 @@ for s in $STEPS; do
     plainprobe) # per-shape own vs vendor plain GEMMs (tools/plain_gemm_probe.py)
       timeout -k 10 400 python -u tools/plain_gemm_probe.py > gpurun_out/plainprobe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/plainprobe_${TAG}.jsonl; exit 1; }
       cat gpurun_out/plainprobe_${TAG}.jsonl ;;
+    cfgs)    # C1 / C4 bf16 / C4 fp8 bench lines (tools/cfg_runs.sh)
+      TAG=$TAG timeout -k 10 1100 bash tools/cfg_runs.sh > gpurun_out/cfgs_${TAG}.txt 2>&1 || { tail -30 gpurun_out/cfgs_${TAG}.txt; exit 1; }
+      cat gpurun_out/cfgs_${TAG}.txt ;;
+    fp8lib)  # C4 fp8 with / without the vendor fp8 GEMMs (tools/fp8_lib_ab.sh)
+      timeout -k 10 1100 bash tools/fp8_lib_ab.sh > gpurun_out/fp8lib_${TAG}.txt 2>&1 || { tail -30 gpurun_out/fp8lib_${TAG}.txt; exit 1; }
+      cat gpurun_out/fp8lib_${TAG}.txt ;;
+    fp8probe) # C4 fp8 shapes own vs vendor (tools/fp8_vendor_probe.py)
+      timeout -k 10 300 python -u tools/fp8_vendor_probe.py > gpurun_out/fp8probe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/fp8probe_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/fp8probe_${TAG}.jsonl ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
