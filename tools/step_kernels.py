@@ -20,7 +20,8 @@ from collections import defaultdict
 
 
 def cat(n):
-    return ('gemm wgrad' if 'wgrad' in n else 'gemm' if 'gemm' in n else 'attn' if 'attn_' in n else
+    return ('gemm wgrad' if 'wgrad' in n else 'gemm' if 'gemm' in n else
+            'gemm (hipBLASLt)' if n.startswith(('Cijk_', 'Custom_Cijk')) else 'attn' if 'attn_' in n else
             'ln' if 'ln_' in n else 'adamw/cast' if ('adamw' in n or 'cast_multi' in n) else
             'colsum' if 'colsum' in n or 'vec_sum' in n else
             'torch' if 'at::native' in n or 'rocclr' in n else 'mae/other')
