@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -393,6 +394,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--sync-loss", action="store_true",
+                    help="read each step's loss before queueing the next (default: once the next step is queued)")
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one HIP graph per step")
     ap.add_argument("--gemm-table", action="store_true", help="per-shape GEMM times to stderr")
     ap.add_argument("--dp", action="store_true",
@@ -487,12 +490,23 @@ def main():
     torch.cuda.synchronize()
     timer.active = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    losses = []
+    for i in range(args.steps):
         loss = step()
         timer.snapshot()
-        runner.loss_value()  # main.py:64 reads the loss every step (published by the step, no copy launch)
+        # main.py:64 reads the loss every step; here step k's value (published by
+        # the step into mapped host memory, no copy launch) is read once step k + 1
+        # is queued, so the host's turnaround does not idle the GPU between steps
+        # (--sync-loss: read each step's own loss before queueing the next)
+        if args.sync_loss:
+            losses.append(runner.loss_value())
+        elif i > 0:
+            losses.append(runner.previous_loss())
+    if not args.sync_loss:
+        losses.append(runner.loss_value())   # the last step's, after it finished
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    assert len(losses) == args.steps and all(math.isfinite(v) for v in losses), losses
     timer.harvest()
     timer.active = False
     if use_dp:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 8
+#define MAECLIP_ABI_VERSION 9
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -525,6 +525,10 @@ int32_t maeclip_host_mapped_alloc(int64_t bytes, void** host_ptr, void** dev_ptr
 int32_t maeclip_host_mapped_free(void* host_ptr);
 /* dst[0..n) = src[0..n) (f32, small n; dst may be device-mapped host memory) */
 int32_t maeclip_copy_f32(const float* src, float* dst, int64_t n, void* stream);
+/* dst[(counter[0] & 1) n + i] = src[i]: the step's loss into one of two host
+ * slots picked by the device step counter, so the host can read step k's value
+ * while step k + 1 (writing the other slot) is already running */
+int32_t maeclip_copy_f32_slot(const float* src, float* dst, int64_t n, const int64_t* counter, void* stream);
 /* dst_i[k] = w * s[0] * src_i[k] (src_i NULL: w * s[0]) for two dense f32
  * arrays in one launch (n_i = 0: unused); src_i == dst_i allowed. The
  * backward of a loss that scales stored gradients by the incoming grad_output

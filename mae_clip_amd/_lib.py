@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -195,6 +195,7 @@ _SIGS = {
     "maeclip_host_mapped_alloc": (c_i32, [C.c_int64, C.POINTER(c_vp), C.POINTER(c_vp)]),
     "maeclip_host_mapped_free": (c_i32, [c_vp]),
     "maeclip_copy_f32": (c_i32, [c_vp, c_vp, C.c_int64, c_vp]),
+    "maeclip_copy_f32_slot": (c_i32, [c_vp, c_vp, C.c_int64, c_vp, c_vp]),
     "maeclip_gemm_impl": (c_i32, [C.POINTER(GemmArgs)]),
     "maeclip_scale_by_scalar2": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, C.c_float, c_vp]),
     "maeclip_memcpy_h2d": (c_i32, [c_vp, c_vp, c_sz, c_vp]),

@@ -510,6 +510,22 @@ extern "C" int32_t maeclip_copy_f32(const float* src, float* dst, int64_t n, voi
   return 0;
 }
 
+__global__ void __launch_bounds__(NTH) copy_f32_slot_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                             int64_t n, const int64_t* __restrict__ counter) {
+  float* d = dst + (counter[0] & 1) * n;
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += (int64_t)gridDim.x * NTH) d[i] = src[i];
+}
+
+extern "C" int32_t maeclip_copy_f32_slot(const float* src, float* dst, int64_t n, const int64_t* counter, void* stream) {
+  MC_CHECK_ARG(n >= 0 && (n == 0 || (src && dst && counter)), "maeclip_copy_f32_slot: bad args");
+  if (n == 0) return 0;
+  const int64_t nb = (n + NTH - 1) / NTH;
+  hipLaunchKernelGGL(copy_f32_slot_kernel, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(NTH), 0, (hipStream_t)stream,
+                     src, dst, n, counter);
+  MC_CHECK_LAUNCH("maeclip_copy_f32_slot");
+  return 0;
+}
+
 extern "C" int32_t maeclip_host_mapped_alloc(int64_t bytes, void** host_ptr, void** dev_ptr) {
   MC_CHECK_ARG(bytes > 0 && host_ptr && dev_ptr, "maeclip_host_mapped_alloc: bad args");
   void* h = nullptr;

@@ -52,6 +52,7 @@ class CapturedStep:
         self.state_key = None
         self._host = None   # kernels.HostScalars: the loss, published inside the step (loss_value)
         self._last = None
+        self._done = []     # (end-of-step event, model.step) of the last two steps queued
 
     def _state_key(self):
         """What a replay bakes in besides the batch: every parameter's storage
@@ -78,23 +79,50 @@ class CapturedStep:
     def _publish(self, loss):
         """write the loss into pinned, device-mapped host memory from inside the
         step (a kernel of the step itself, captured with it), so that the host's
-        per-step read (main.py:64) needs no device-to-host copy launch"""
+        per-step read (main.py:64) needs no device-to-host copy launch. Two
+        slots, picked by the model's device step counter: step c writes slot
+        c & 1, so step c's value can be read while step c + 1 runs."""
         self._last = loss.detach()
         if not loss.is_cuda:
             return
+        counter = getattr(self.model, "step_counter", None)
+        slot_ok = torch.is_tensor(counter) and counter.is_cuda and counter.dtype == torch.int64
         if self._host is None:
             from . import kernels as K
-            self._host = K.HostScalars(1)
-        self._host.publish(loss.detach().reshape(1).float())
+            self._host = K.HostScalars(1, slots=2 if slot_ok else 1)
+        self._host.publish(loss.detach().reshape(1).float(), counter if slot_ok else None)
+
+    def _slot(self, c):
+        return (c & 1) if self._host is not None and self._host.slots == 2 else 0
+
+    def _mark(self):
+        """after a step is queued: an event at its end and its step count"""
+        if self._host is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._done.append((ev, int(getattr(self.model, "step", 0))))
+            del self._done[:-2]
 
     def loss_value(self) -> float:
         """The last step's loss as a Python float (the reference's loss.item(),
-        main.py:64): waits for the current stream, then reads the value the step
-        published -- no copy kernel."""
-        if self._host is None:
+        main.py:64): waits for that step, then reads the value it published --
+        no copy kernel."""
+        if self._host is None or not self._done:
             return float(self._last.item())
-        torch.cuda.current_stream().synchronize()
-        return self._host.values()[0]
+        ev, c = self._done[-1]
+        ev.synchronize()
+        return self._host.values(self._slot(c))[0]
+
+    def previous_loss(self):
+        """The loss of the step before the last one queued (None after the first
+        step): call it right after step() to read step k's loss while step k + 1
+        runs -- the per-step read of main.py:64 without a GPU bubble at the step
+        boundary (the host's graph launch of step k + 1 is already queued)."""
+        if self._host is None or len(self._done) < 2:
+            return None
+        ev, c = self._done[-2]
+        ev.synchronize()
+        return self._host.values(self._slot(c))[0]
 
     def _eager(self, batch):
         self.opt.zero_grad(set_to_none=True)
@@ -146,6 +174,13 @@ class CapturedStep:
                    and v.device == self.static[k].device for k, v in batch.items()) and len(batch) == len(self.static)
 
     def step(self, batch):
+        """One training step on `batch` (dict of device tensors); returns the loss tensor.
+        (The step is queued; loss_value() / previous_loss() read its published loss.)"""
+        loss = self._step(batch)
+        self._mark()
+        return loss
+
+    def _step(self, batch):
         """One training step on `batch` (dict of device tensors); returns the loss tensor.
 
         A batch whose shapes differ from the captured ones (e.g. the last,

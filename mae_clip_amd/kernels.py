@@ -653,22 +653,29 @@ class HostScalars:
     a kernel writes them on the stream (publish), the host reads them after
     synchronising that stream (values) -- no device-to-host copy launch."""
 
-    def __init__(self, n=1):
-        self.n = int(n)
+    def __init__(self, n=1, slots=1):
+        self.n, self.slots = int(n), int(slots)
         h, d = C.c_void_p(), C.c_void_p()
-        _call("maeclip_host_mapped_alloc", 4 * self.n, C.byref(h), C.byref(d))
+        _call("maeclip_host_mapped_alloc", 4 * self.n * self.slots, C.byref(h), C.byref(d))
         self.host, self.dev = h.value, d.value
-        self._view = (C.c_float * self.n).from_address(self.host)
+        self._view = (C.c_float * (self.n * self.slots)).from_address(self.host)
 
-    def publish(self, src):
-        """copy the first n values of device f32 tensor `src` here (stream-ordered)"""
+    def publish(self, src, counter=None):
+        """copy the first n values of device f32 tensor `src` here (stream-ordered);
+        with `counter` (device int64) into slot counter & 1 of a 2-slot buffer
+        (HostScalars(n, slots=2))"""
         _dev(src)
         if src.dtype != torch.float32 or src.numel() < self.n or not src.is_contiguous():
             raise TypeError("HostScalars.publish: contiguous f32 device tensor with >= n values")
-        _call("maeclip_copy_f32", src.data_ptr(), self.dev, self.n, _stream())
+        if counter is None:
+            _call("maeclip_copy_f32", src.data_ptr(), self.dev, self.n, _stream())
+        else:
+            if self.slots != 2 or counter.dtype != torch.int64:
+                raise TypeError("HostScalars.publish: slot publishing needs slots=2 and an int64 counter")
+            _call("maeclip_copy_f32_slot", src.data_ptr(), self.dev, self.n, counter.data_ptr(), _stream())
 
-    def values(self):
-        return [float(v) for v in self._view]
+    def values(self, slot=0):
+        return [float(v) for v in self._view[slot * self.n:(slot + 1) * self.n]]
 
     def __del__(self):
         try:

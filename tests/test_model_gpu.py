@@ -334,6 +334,35 @@ def _partial_runs(dev, sizes, runs, product_config, kw, CLIPModel, AdamW, Captur
         runs.append((losses, m, runner))
 
 
+@pytest.mark.parametrize("captured", [False, True])
+def test_captured_step_previous_loss(dev, captured):
+    """CapturedStep.previous_loss(): steps queued back to back, step k's loss
+    (published into slot k & 1 of the mapped host buffer) read while step k + 1
+    runs -- bench.py's per-step read -- equals that step's loss; loss_value()
+    gives the last one."""
+    from tests.helpers import product_config, C0
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.optim import AdamW
+    from mae_clip_amd.graph import CapturedStep
+    kw = {k: v for k, v in C0.items() if k != "batch_size"}
+    with product_config(precision="bf16", **kw):
+        torch.manual_seed(0)
+        m = CLIPModel().to(dev).train()
+    opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    runner = CapturedStep(m, opt, enabled=captured)
+    late = []
+    for it in range(7):
+        batch = {k: v.to(dev) for k, v in make_batch(8, 32, seed=it).items()}
+        cur = runner.step(batch)
+        prev = runner.previous_loss()
+        late.append((prev, cur.item()))   # a replay returns the same tensor each time: take its value now
+    assert late[0][0] is None
+    for (p_, _), (_, c_prev) in zip(late[1:], late[:-1]):
+        assert p_ == c_prev, (p_, c_prev)
+    assert runner.loss_value() == late[-1][1]
+    assert len(set(v for _, v in late)) == len(late)
+
+
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_captured_step_matches_eager(dev, precision):
     """mae_clip_amd.graph.CapturedStep (forward+backward+AdamW in one HIP graph,

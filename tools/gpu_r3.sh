@@ -108,6 +108,9 @@ for s in $STEPS; do
     fp8probe) # C4 fp8 shapes own vs vendor (tools/fp8_vendor_probe.py)
       timeout -k 10 300 python -u tools/fp8_vendor_probe.py > gpurun_out/fp8probe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/fp8probe_${TAG}.jsonl; exit 1; }
       cat gpurun_out/fp8probe_${TAG}.jsonl ;;
+    asyncloss) # loss read before / after queueing the next step (tools/async_loss_ab.sh)
+      timeout -k 10 900 bash tools/async_loss_ab.sh > gpurun_out/asyncloss_${TAG}.txt 2>&1 || { tail -30 gpurun_out/asyncloss_${TAG}.txt; exit 1; }
+      cat gpurun_out/asyncloss_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
