@@ -351,8 +351,13 @@ def u8_leg(model, opt, args, size, device, use_graph):
     torch.cuda.synchronize()
     steps = max(1, min(args.steps, 10))
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step().item()
+    for i in range(steps):
+        step()
+        if i > 0 and not args.sync_loss:
+            runner.previous_loss()   # step i-1's loss, read while step i runs (as in the headline loop)
+        elif args.sync_loss:
+            runner.loss_value()
+    runner.loss_value()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     h2d = sum(v.numel() * v.element_size() for v in host.values())
