@@ -111,6 +111,9 @@ for s in $STEPS; do
     asyncloss) # loss read before / after queueing the next step (tools/async_loss_ab.sh)
       timeout -k 10 900 bash tools/async_loss_ab.sh > gpurun_out/asyncloss_${TAG}.txt 2>&1 || { tail -30 gpurun_out/asyncloss_${TAG}.txt; exit 1; }
       cat gpurun_out/asyncloss_${TAG}.txt ;;
+    boundary) # GPU idle time between two replays of the captured step (tools/step_boundary_ab.sh)
+      timeout -k 10 1500 bash tools/step_boundary_ab.sh > gpurun_out/boundary_${TAG}.txt 2>&1 || { tail -30 gpurun_out/boundary_${TAG}.txt; exit 1; }
+      grep -v "^\[" gpurun_out/boundary_${TAG}.txt ;;
     *)
       echo "unknown step $s"; exit 2 ;;
   esac
