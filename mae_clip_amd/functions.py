@@ -18,6 +18,7 @@ Reference ops replaced (file:line):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -202,6 +203,22 @@ class MicroBatches:
         self.rows = [(i * self.Bs * n, (i + 1) * self.Bs * n) for i in range(S)]
         self.main = torch.cuda.current_stream(device)
         self.streams = [self.main] + [mb_stream(device, i) for i in range(1, S)]
+        # stagger (A/B, MAECLIP_MB_STAGGER=k): micro-batch i > 0 starts a block only
+        # after micro-batch i - 1 has issued k launches of it, so that different
+        # kernels of the block (GEMM epilogues vs attention / LayerNorm) coincide
+        self.stagger = int(os.environ.get("MAECLIP_MB_STAGGER", "0") or 0)
+        self._ticks = 0
+        self._gate = None
+
+    def tick(self):
+        """after each launch of a block: records the stagger gate on the
+        micro-batch's stream after its k-th launch"""
+        if self.stagger <= 0:
+            return
+        self._ticks += 1
+        if self._ticks == self.stagger:
+            self._gate = torch.cuda.Event()
+            self._gate.record()
 
     def fork(self):
         for st in self.streams[1:]:
@@ -216,6 +233,9 @@ class MicroBatches:
         for i, st in enumerate(self.streams):
             r0, r1 = self.rows[i]
             _MB_ACTIVE[0] = i
+            if self._gate is not None:
+                st.wait_event(self._gate)
+            self._ticks, self._gate = 0, None
             try:
                 with torch.cuda.stream(st):
                     yield i, slice(r0, r1), slice(i * self.Bs, (i + 1) * self.Bs)
@@ -317,12 +337,18 @@ class TransformerStackFn(torch.autograd.Function):
             for mi, rs, bs in mb.each():
                 xr = xin[mi]
                 K.ln_fwd(xr, n1w, n1b, spec.eps, out_dtype=T, y_out=h1[rs], mean_out=m1[rs], rstd_out=r1[rs])
+                mb.tick()
                 K.linear_fwd(h1[rs], wqkv, bias=bqkv, out=qkv[rs])
+                mb.tick()
                 K.attn_fwd(qkv[rs], mb.Bs, n, H, hd, scale, o_out=o[rs], lse_out=lse[bs])
+                mb.tick()
                 K.linear_fwd(o[rs], wproj, bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xr,
                              out=x1[rs])
+                mb.tick()
                 K.ln_fwd(x1[rs], n2w, n2b, spec.eps, out_dtype=T, y_out=h2[rs], mean_out=m2[rs], rstd_out=r2[rs])
+                mb.tick()
                 K.linear_fwd(h2[rs], w1, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu[rs], out=a[rs])
+                mb.tick()
                 K.linear_fwd(a[rs], w2, bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1[rs],
                              out=outs[i][rs])
                 xin[mi] = outs[i][rs]
@@ -460,14 +486,20 @@ class TransformerStackFn(torch.autograd.Function):
                 cs = slice(rs.start // 64, rs.stop // 64)
                 K.linear_dgrad(gTs, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu[rs], colsum=b["dA_part"][cs],
                                out=b["dA"][rs])
+                mb.tick()
                 K.linear_dgrad(b["dA"][rs], w1, out=b["dh2"][rs])
+                mb.tick()
                 K.ln_bwd(b["dh2"][rs], x1[rs], m2[rs], r2[rs], n2w, dres=gs, want_bf16=True, want_colsum=True,
                          dx_out=b["dx1"][rs], dxb_out=b["dx1T"][rs], pg_out=b["pg2"][ps], pb_out=b["pb2"][ps],
                          pc_out=b["pc2"][ps])
+                mb.tick()
                 K.linear_dgrad(b["dx1T"][rs], wproj, out=b["dO"][rs])
+                mb.tick()
                 K.attn_bwd(qkv[rs], o[rs], b["dO"][rs], lse[bs], mb.Bs, n, H, hd, scale,
                            dqkv_out=b["dqkv"][rs], part_out=b["qpart"][bs])
+                mb.tick()
                 K.linear_dgrad(b["dqkv"][rs], wqkv, out=b["dh1"][rs])
+                mb.tick()
                 K.ln_bwd(b["dh1"][rs], xi[rs], m1[rs], r1[rs], n1w, dres=b["dx1"][rs], want_bf16=True,
                          want_colsum=True, dx_out=b["dx"][rs], dxb_out=b["dxT"][rs], pg_out=b["pg1"][ps],
                          pb_out=b["pb1"][ps], pc_out=b["pc1"][ps])
