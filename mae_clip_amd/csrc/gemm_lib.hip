@@ -55,6 +55,13 @@ struct LibPlan {
   hipblasLtMatmulAlgo_t algo;
   size_t ws = 0;
   bool ok = false;
+  // the heuristic's candidates (MAECLIP_GEMM_LIB_TUNE: the fastest of them,
+  // timed once on the first call outside a graph capture)
+  static constexpr int NCAND = 16;
+  hipblasLtMatmulAlgo_t cand[NCAND];
+  size_t cand_ws[NCAND] = {};
+  int ncand = 0;
+  bool tuned = false;
 };
 
 struct LibState {
@@ -73,8 +80,14 @@ int lib_mode() {
   return (e && *e) ? atoi(e) : 1;
 }
 
+// MAECLIP_GEMM_LIB_TUNE=1: time the heuristic's candidates once per shape
+bool tune_on() {
+  const char* e = getenv("MAECLIP_GEMM_LIB_TUNE");
+  return e && *e == '1';
+}
+
 // plan (descriptors + the heuristic's first algorithm) of one shape, cached per device
-const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws, const float* scale_a = nullptr,
+LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws, const float* scale_a = nullptr,
                         const float* scale_b = nullptr) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
@@ -133,14 +146,20 @@ const LibPlan* plan_for(const maeclip_gemm_args& a, bool have_ws, const float* s
     ok = hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
          hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)) ==
              HIPBLAS_STATUS_SUCCESS;
-    hipblasLtMatmulHeuristicResult_t hr[1];
+    hipblasLtMatmulHeuristicResult_t hr[LibPlan::NCAND];
     int n = 0;
-    ok = ok && hipblasLtMatmulAlgoGetHeuristic(st.handle[dev], p.desc, p.la, p.lb, res ? p.lr : p.lc, p.lc, pref, 1, hr,
-                                               &n) == HIPBLAS_STATUS_SUCCESS && n > 0 && hr[0].state == HIPBLAS_STATUS_SUCCESS;
+    ok = ok && hipblasLtMatmulAlgoGetHeuristic(st.handle[dev], p.desc, p.la, p.lb, res ? p.lr : p.lc, p.lc, pref,
+                                               tune_on() ? LibPlan::NCAND : 1, hr, &n) == HIPBLAS_STATUS_SUCCESS &&
+         n > 0 && hr[0].state == HIPBLAS_STATUS_SUCCESS;
     if (ok) {
       p.algo = hr[0].algo;
       p.ws = hr[0].workspaceSize;
       ok = p.ws <= (size_t)wsb;
+      for (int i = 0; i < n && i < LibPlan::NCAND; ++i)
+        if (hr[i].state == HIPBLAS_STATUS_SUCCESS && hr[i].workspaceSize <= (size_t)wsb) {
+          p.cand[p.ncand] = hr[i].algo;
+          p.cand_ws[p.ncand++] = hr[i].workspaceSize;
+        }
     }
     if (pref) hipblasLtMatmulPreferenceDestroy(pref);
   }
@@ -184,12 +203,13 @@ int64_t gemm_lib_workspace(const maeclip_gemm_args& a) { return (gemm_lib_ok(a) 
 // library's own kernels)
 int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a, const float* scale_b) {
   const bool have_ws = a.workspace != nullptr;
-  const LibPlan* p = plan_for(a, have_ws, scale_a, scale_b);
+  LibPlan* p = plan_for(a, have_ws, scale_a, scale_b);
   if (!p) return 1;
   int dev = 0;
   (void)hipGetDevice(&dev);
   const bool res = a.epilogue == 2;
   const float alpha = a.alpha, beta = res ? 1.f : 0.f;
+
   if (a.bias) {
     const void* bp = a.bias;
     MC_CHECK_ARG(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)) ==
@@ -203,6 +223,38 @@ int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a, co
                      hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &sq, sizeof(sq)) ==
                          HIPBLAS_STATUS_SUCCESS,
                  "maeclip_gemm_fp8: hipBLASLt scale pointers");
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (!p->tuned && p->ncand > 1 && have_ws && (!res || (const void*)a.resid != a.C) &&
+      hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    // on this call's own operands (the final call below rewrites the outputs),
+    // with the device drained first so that no other stream's kernels co-run
+    hipEvent_t e0, e1;
+    if (hipDeviceSynchronize() == hipSuccess && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+      float best = 1e30f;
+      int bi = 0;
+      for (int i = 0; i < p->ncand; ++i) {
+        bool good = true;
+        for (int r = 0; r < 4 && good; ++r) {
+          if (r == 1) good = hipEventRecord(e0, s) == hipSuccess;
+          good = good && hipblasLtMatmul(state().handle[dev], p->desc, &alpha, a.B, p->la, a.A, p->lb, &beta,
+                                         res ? (const void*)a.resid : a.C, res ? p->lr : p->lc, a.C, p->lc,
+                                         &p->cand[i], (void*)a.workspace, p->cand_ws[i], s) == HIPBLAS_STATUS_SUCCESS;
+        }
+        float ms = 0.f;
+        good = good && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+               hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+        if (good && ms < best) {
+          best = ms;
+          bi = i;
+        }
+      }
+      p->algo = p->cand[bi];
+      p->ws = p->cand_ws[bi];
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
+    p->tuned = true;
   }
   const hipblasStatus_t r = hipblasLtMatmul(state().handle[dev], p->desc, &alpha, a.B, p->la, a.A, p->lb, &beta,
                                             res ? (const void*)a.resid : a.C, res ? p->lr : p->lc, a.C, p->lc, &p->algo,
