@@ -112,6 +112,47 @@ def parity_headline(device, precision="bf16", B=4):
     return abs(lp - lr), abs(lp - lr) / max(1.0, abs(lr)), lp, lr
 
 
+def train_curve_headline(device, precision="bf16", B=4, steps=5):
+    """The reference's train loop (main.py:54-66: forward, zero_grad, backward,
+    AdamW(lr 1e-3, wd 1e-3) step, main.py:101-103) for `steps` steps at the
+    metric's model shapes (ViT-B/16 @224, mask .75, 8x512 decoder, 6-layer
+    text) in TRAIN mode: the product at `precision` with its fused AdamW vs the
+    fp64 CPU oracle with torch.optim.AdamW, identical initial weights, batches
+    and MAE masks (both advance the mask step every training forward). Dropout
+    is set to 0 on both sides (the two RNG streams cannot match)."""
+    sys.path.insert(0, ROOT)
+    from tests.helpers import build_pair, make_batch
+    from mae_clip_amd.optim import AdamW
+    kw = dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6, mask_ratio=0.75,
+              decoder_embed_dim=512, decoder_depth=8, decoder_num_heads=16, dropout=0.0, text_dropout=0.0,
+              text_attention_dropout=0.0)
+    prod, ref = build_pair(precision, **kw)
+    for m in ref.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    prod.train()
+    ref.train()
+    opt_p = AdamW([p for p in prod.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    opt_r = torch.optim.AdamW([p for p in ref.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+    rows = []
+    for k in range(steps):
+        b = make_batch(B, 224, seed=40 + k)
+        lp = prod({kk: v.to(device) for kk, v in b.items()})
+        opt_p.zero_grad()
+        lp.backward()
+        opt_p.step()
+        lr = ref(dict(b, image=b["image"].double()))
+        opt_r.zero_grad()
+        lr.backward()
+        opt_r.step()
+        lpv, lrv = lp.item(), lr.item()
+        rows.append({"step": k, "product": lpv, "oracle": lrv, "rel": abs(lpv - lrv) / max(1.0, abs(lrv))})
+    return {"precision": precision, "steps": steps, "batch": B, "worst_rel": max(r["rel"] for r in rows),
+            "last_rel": rows[-1]["rel"], "curve": rows,
+            "config": "C2 model shapes, train mode (dropout 0 both sides), AdamW lr 1e-3 wd 1e-3 (main.py:54-66, "
+                      ":101-103) vs the fp64 CPU oracle + torch.optim.AdamW"}
+
+
 def cpu_model_name():
     try:
         for line in open("/proc/cpuinfo"):
@@ -528,11 +569,25 @@ def main():
     assert len(losses) == args.steps and all(math.isfinite(v) for v in losses), losses
     timer.harvest()
     timer.active = False
+    # the drop-in loop as main.py:64 runs it: each step's loss read (blocking)
+    # before the next step is queued; reported beside the headline, not as value
+    sync_el = None
+    if not args.sync_loss:
+        if use_dp:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step()
+            assert math.isfinite(runner.loss_value())
+        torch.cuda.synchronize()
+        sync_el = time.perf_counter() - t1
     if use_dp:
         dist.barrier()
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, sync_el or 0.0], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = t[0].item()
+        sync_el = t[1].item() if sync_el is not None else None
     global_batch = args.batch * world
     value = global_batch * args.steps / elapsed
     ms = elapsed / args.steps * 1000.0
@@ -565,6 +620,15 @@ def main():
                           "img_flops": img_flops},
                "loss": round(loss.item(), 4), "roofline": roof, "roofline_fwd_dgrad": roof2,
                "u8_input_pipeline": u8,
+               "loss_read": ("sync: each step's loss read before the next step is queued (main.py:64)"
+                             if args.sync_loss else
+                             "pipelined: step k's loss (published by the step into mapped host memory) read right "
+                             "after step k+1 is queued; every step's loss is read"),
+               "sync_loss_leg": None if sync_el is None else {
+                   "value": round(global_batch * args.steps / sync_el, 2), "unit": "images/s",
+                   "ms_per_step": round(sync_el / args.steps * 1000.0, 3), "steps": args.steps,
+                   "what": "the same captured step, each step's loss read (blocking) before the next is queued, "
+                           "as main.py:64's loss.item() does"},
                "step_mode": "hip-graph" if use_graph else "eager",
                "rccl": {"backend": dist.get_backend(), "world_size": dist.get_world_size()} if use_dp else None}
         if world == 1 and not args.no_parity:
@@ -584,6 +648,12 @@ def main():
                                   "eval-mode forward vs the fp64 CPU oracle", "seconds": round(time.time() - t0, 1)}
                 except Exception as e:
                     out["loss_delta_vs_ref_headline"] = {"error": repr(e)}
+                try:
+                    t0 = time.time()
+                    out["train_curve_vs_ref_headline"] = dict(train_curve_headline(device, args.precision),
+                                                              seconds=round(time.time() - t0, 1))
+                except Exception as e:
+                    out["train_curve_vs_ref_headline"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         sys.stdout.flush()

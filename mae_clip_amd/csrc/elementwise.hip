@@ -464,8 +464,9 @@ __global__ void counter_add_kernel(int64_t* c, int64_t delta, int64_t* snap) {
 __global__ void scalar_axpy_kernel(const float* a, const float* b, float w, float* out) {
   if (threadIdx.x == 0) out[0] = fmaf(w, b[0], a[0]);
 }
-__global__ void __launch_bounds__(NTH) scale2_kernel(const float* __restrict__ s0, float* __restrict__ d0, int64_t n0,
-                                                     const float* __restrict__ s1, float* __restrict__ d1, int64_t n1,
+// src_i == dst_i (in place) is allowed, so the src / dst pairs are not __restrict__
+__global__ void __launch_bounds__(NTH) scale2_kernel(const float* s0, float* d0, int64_t n0,
+                                                     const float* s1, float* d1, int64_t n1,
                                                      const float* __restrict__ sc, float w, int64_t nb0) {
   const float f = w * sc[0];
   const bool second = blockIdx.x >= nb0;

@@ -464,7 +464,119 @@ struct Unit4 {
   int kbeg, nt;       // first k and number of 64-wide K-tiles of this unit
   int slice, prob;
   int slot;           // stream-K partial tile: workspace slot; -1 = final result
+  int tl;             // stream-K: remainder tile index
 };
+
+// Stream-K plan of a plain launch (maeclip_gemm with a workspace): tiles
+// [0, Tdp) run whole on the persistent grid (Tdp a multiple of it); the
+// K-tiles of the R = T - Tdp remainder tiles are dealt out skw per block in
+// XCD-contiguous block-position order, so every block does the same work and
+// a launch with fewer tiles than CUs still fills the chip (the micro-batch's
+// 6400-row encoder shapes: 75 tiles of 256 x 256 for 256 CUs). A block's
+// range cuts at most two tiles: its first and its last. The pieces of a cut
+// tile are summed IN THE SAME LAUNCH by the block that arrives last
+// (sk_fixup): no second launch, no waiting, a fixed summation order.
+// Workspace: [SK_CNT_BYTES] arrival counters (zero before the first launch,
+// left zero by every completed launch), then 2 slots of SK_SLOT bytes per block.
+constexpr int SK_CNT_STRIDE = 16;                 // counter words apart (64 B)
+constexpr int64_t SK_CNT_BYTES = 256 * SK_CNT_STRIDE * 4;
+constexpr int64_t SK_SLOT = 256 * 256 * 4;        // one fp32 256x256 tile
+struct SkPlan {
+  int Tdp, skw, NT;   // skw = 0: no stream-K
+  unsigned* cnt;
+  float* slots;
+};
+struct Gemm4Args {
+  maeclip_gemm_args a;
+  SkPlan sk;
+  const float* sa;    // fp8 only: per-row A / per-column B dequantisation scales
+  const float* sb;
+};
+
+// Fix-up of one cut tile (stream-K piece `piece` of `np`): returns true in the
+// block that arrives last, whose acc then holds the whole tile's sum and which
+// runs the epilogue. Hand-off (MI355X_MICROARCH.md, valid forms, first row of
+// the sc1 table): every piece is stored write-through (16-B sc1 stores), each
+// storing wave drains with vmcnt(0), a workgroup barrier, then ONE lane adds to
+// the tile's agent-scope counter; the block whose add returns np - 1 (or whose
+// sc1 poll already reads np - 1 and so skips its own store) reads the other
+// pieces with sc1 loads only. The summation order is fixed by piece index
+// whichever block reduces: ((p0 + p1) + p2) + ..., the reducer's own partial
+// entering at its position, so the output bits do not depend on arrival order.
+// Slot layout is fragment-native (the accumulator registers as they stand, 1
+// KiB per wave-instruction): [wave][row fragment][col fragment][lane] x 16 B.
+template <int NF>
+__device__ __forceinline__ bool sk_fixup(v4f (&acc)[NF][4], const SkPlan& sk, const Unit4& u, int skp, int G,
+                                         int* flag, int tid, int wave, int lane) {
+  // pieces p_first .. p_last (block positions) of remainder tile u.tl
+  const int NT = sk.NT, w = sk.skw;
+  const int p_first = u.tl * NT / w, np = ((u.tl + 1) * NT - 1) / w - p_first + 1;
+  unsigned* cnt = sk.cnt + u.tl * SK_CNT_STRIDE;
+  const unsigned last_count = (unsigned)(np - 1);
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sk.slots, (short)0, (int)(2 * (int64_t)G * SK_SLOT),
+                                                      0x00020000);
+  const int vo = lane * 16 + wave * NF * 4 * 1024;
+  if (tid == 0) *flag = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last_count ? 1 : 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  SEG_BARRIER();
+  bool last = *flag == 1;
+  if (!last) {
+    const int so = skp * 2 * (int)SK_SLOT + (u.slot & 1) * (int)SK_SLOT;
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rs, vo + (i * 4 + j) * 1024, so, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SEG_BARRIER();
+    if (tid == 0)
+      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last_count ? 1 : 2;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SEG_BARRIER();
+    last = *flag == 1;
+  }
+  if (!last) return false;
+  // the pieces' slots: piece p is held by block position bp = p_first + p, in
+  // its first (slot 0) or last (slot 1) job
+  auto slot_off = [&](int p) {
+    const int bp = p_first + p;
+    return bp * 2 * (int)SK_SLOT + ((int)((int64_t)bp * w / NT) == u.tl ? 0 : (int)SK_SLOT);
+  };
+  const int r = skp - p_first;
+#ifndef SKX_NO_REDUCE
+  // one row fragment (4 accumulators) at a time: (p_0 + ... + p_{r-1}) + own,
+  // then + p_{r+1} + ... in order
+  auto ld4 = [&](int p, int i, v4f (&L)[4]) {
+    const int so = slot_off(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      L[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + (i * 4 + j) * 1024, so, 16));
+  };
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    if (r > 0) {
+      v4f T[4];
+      ld4(0, i, T);
+      for (int p = 1; p < r; ++p) {
+        v4f L[4];
+        ld4(p, i, L);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) T[j] += L[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = T[j] + acc[i][j];
+    }
+    for (int p = r + 1; p < np; ++p) {
+      v4f L[4];
+      ld4(p, i, L);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += L[j];
+    }
+  }
+#endif
+  if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
 
 // Grouped weight gradients (maeclip_wgrad_grouped): dW_p[N_p, K_p] (+)=
 // dy_p[Mtok, N_p]^T x_p[Mtok, K_p] for up to WG_MAX problems in one persistent
@@ -495,12 +607,13 @@ struct WgGroup {
 // F8: 0 = bf16 operands (K-tile 64); 1 / 2 = fp8 operands, A e4m3 / e5m2 and
 // B e4m3 (K-tile 128 = the same 128 bytes per row), per-row A scales sa[M] and
 // per-column B scales sb[N] applied in the epilogue.
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256>
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256, bool SK = false>
 __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp,
                                            const float* __restrict__ sa = nullptr,
-                                           const float* __restrict__ sb = nullptr) {
+                                           const float* __restrict__ sb = nullptr, const SkPlan* skp_ = nullptr) {
   static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
   static_assert(BM == 256 || (BM == 192 && LA == LAY_KC && !SPLIT && !GRP), "BM 192: KC A, plain launches only");
+  static_assert(!SK || (!SPLIT && !GRP), "stream-K: plain launches only");
   using TM = TileM<BM>;
   constexpr int MI = TM::MI;
   constexpr int ESZ = F8 ? 1 : 2;      // operand bytes per element
@@ -524,6 +637,20 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     T = gm * gn;
     const int S = SPLIT ? args.splitk : 1;
     klen = (((int)args.K + S - 1) / S + KT - 1) / KT * KT;
+  }
+  // stream-K remainder (grouped: gp; plain launches: *skp_): tiles [Tdp, Ttot)
+  // are dealt out by K-tiles, skw per block
+  int Ttot = T, Tdp = T, skw = 0, NTr = 1;
+  if (GRP && gp->skw > 0) {
+    Ttot = gp->T;
+    Tdp = gp->Tdp;
+    skw = gp->skw;
+    NTr = gp->NT;
+  }
+  if (SK) {
+    Tdp = T = skp_->Tdp;
+    skw = skp_->skw;
+    NTr = skp_->NT;
   }
   auto unit = [&](int u) {
     Unit4 w;
@@ -576,24 +703,37 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   // this block's jobs: its whole tiles, then (grouped stream-K) its K range of
   // the remainder tiles
   const int ndp = cbeg + li < cend ? (cend - (cbeg + li) + nbx - 1) / nbx : 0;
-  int ska = 0, skb = 0, nsk = 0, skp = 0;
-  if (GRP && gp->skw > 0) {
+  // this block's stream-K range [ska, skb) of (remainder tile, K-tile)
+  // iterations: tiles t0 (from K-tile k0) .. t1 (up to K-tile k1); the
+  // divisions stay out of the K loop, where job() is also called
+  int nsk = 0, skp = 0, sk_t0 = 0, sk_k0 = 0, sk_t1 = 0, sk_k1 = 0;
+  if (skw > 0) {
     skp = G % 8 == 0 ? x8 * (G / 8) + li : (int)blockIdx.x;   // XCD-contiguous positions
-    const int tot = (gp->T - gp->Tdp) * gp->NT;
-    ska = min(skp * gp->skw, tot);
-    skb = min(ska + gp->skw, tot);
-    nsk = skb > ska ? (skb - 1) / gp->NT - ska / gp->NT + 1 : 0;
+    const int tot = (Ttot - Tdp) * NTr;
+    const int ska = min(skp * skw, tot), skb = min(ska + skw, tot);
+    if (skb > ska) {
+      sk_t0 = ska / NTr;
+      sk_k0 = ska - sk_t0 * NTr;
+      sk_t1 = (skb - 1) / NTr;
+      sk_k1 = skb - sk_t1 * NTr;
+      nsk = sk_t1 - sk_t0 + 1;
+    }
   }
   auto job = [&](int j) -> Unit4 {
-    if (j < ndp) return unit(cbeg + li + j * nbx);
-    const int s = j - ndp, NT = gp->NT;
-    const int tl = ska / NT + s;
-    const int k0 = s == 0 ? ska % NT : 0;
-    const int k1 = tl == (skb - 1) / NT ? (skb - 1) % NT + 1 : NT;
-    Unit4 w = unit(gp->Tdp + tl);
+    if (j < ndp) {
+      Unit4 w = unit(cbeg + li + j * nbx);
+      w.tl = 0;
+      return w;
+    }
+    const int s = j - ndp, NT = NTr;
+    const int tl = sk_t0 + s;
+    const int k0 = s == 0 ? sk_k0 : 0;
+    const int k1 = tl == sk_t1 ? sk_k1 : NT;
+    Unit4 w = unit(Tdp + tl);
     w.kbeg = k0 * KT;
     w.nt = k1 - k0;
     w.slot = (k0 == 0 && k1 == NT) ? -1 : 2 * skp + (s == 0 ? 0 : 1);
+    w.tl = tl;
     return w;
   };
   const int njobs = ndp + nsk;
@@ -779,7 +919,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     }
     if (nt == 0 && wm == 0) SEG_BARRIER();
     STAMP(2);
-    if constexpr (BM != 256) {
+    // cut tile (stream-K): the epilogue runs once, in the block that sums the
+    // pieces (one epilogue call site either way). Flag word: the Am1 half of
+    // LDS buffer 1, which no DMA writes before the next unit's first K-tile
+    // (the prologue fills buffer 0 and the other three halves of buffer 1)
+    bool run_epi = true;
+    if (SK && u.slot >= 0)
+      run_epi = sk_fixup<2 * MI>(acc, *skp_, u, skp, G, (int*)(smem + TM::BUF_T + TM::HALF_A), tid, wave, lane);
+    if (!run_epi) {
+    } else if constexpr (BM != 256) {
       epilogue4<OutT, EPI, F8 != 0, BM>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
     } else if (GRP) {
       const WgProb& q = gp->p[u.prob];
@@ -810,20 +958,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   }
 }
 
-template <int LA, int LB, typename OutT, int EPI, bool SPLIT, int BM = 256>
-__global__ void __launch_bounds__(512) gemm4_kernel(const maeclip_gemm_args args) {
-  gemm4_body<LA, LB, OutT, EPI, SPLIT, false, 0, BM>(args, nullptr);
+template <int LA, int LB, typename OutT, int EPI, bool SPLIT, int BM = 256, bool SK = false>
+__global__ void __launch_bounds__(512) gemm4_kernel(const Gemm4Args g) {
+  gemm4_body<LA, LB, OutT, EPI, SPLIT, false, 0, BM, SK>(g.a, nullptr, nullptr, nullptr, &g.sk);
 }
 
 // fp8 operands (maeclip_gemm_fp8): KC x KC, per-row / per-column scales
-struct Gemm8Args {
-  maeclip_gemm_args a;
-  const float* sa;
-  const float* sb;
-};
-template <typename OutT, int EPI, int F8, int BM = 256>
-__global__ void __launch_bounds__(512) gemm4_f8_kernel(const Gemm8Args g) {
-  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8, BM>(g.a, nullptr, g.sa, g.sb);
+template <typename OutT, int EPI, int F8, int BM = 256, bool SK = false>
+__global__ void __launch_bounds__(512) gemm4_f8_kernel(const Gemm4Args g) {
+  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8, BM, SK>(g.a, nullptr, g.sa, g.sb, &g.sk);
 }
 
 // grouped weight gradients: RC x RC, fp32 out, no epilogue (beta only)
@@ -893,18 +1036,67 @@ int gemm4_ncu() {
   return cap > 0 && cap < ncu ? cap : ncu;
 }
 
-// 192-row tiles when they need fewer full-tile rounds of the persistent grid;
-// MAECLIP_GEMM_BM=256 / 192 forces one (A/B, tests)
-bool use_bm192(const maeclip_gemm_args& a, int ncu) {
-  const char* e = getenv("MAECLIP_GEMM_BM");   // 256 / 192: force (A/B, tests)
-  const int force = (e && *e) ? atoi(e) : 0;
-  if (force == 256 || a.a_layout != LAY_KC || a.splitk > 1 || a.batch > 1 || a.colsum_partial) return false;
-  const int64_t gn = (a.N + 255) / 256;
-  const int64_t t256 = (a.M + 255) / 256 * gn, t192 = (a.M + 191) / 192 * gn;
-  if (force == 192) return true;
-  // measured: a 192-row tile costs ~0.89 of a 256-row one (encoder fc2 fwd, 1 round each)
-  const double r256 = (double)((t256 + ncu - 1) / ncu), r192 = 0.89 * (double)((t192 + ncu - 1) / ncu);
-  return r192 < r256 - 1e-9;
+// Tile height and stream-K plan of a plain launch (one batch, no split-K),
+// from a cost model in units of one 256-row K-tile (~2.9k cycles, 64 KiB of
+// operand DMA per CU): a 192-row K-tile costs 0.89 of it (measured, encoder fc2
+// fwd, one round each); a tile's epilogue ~EPI_C; a stream-K fix-up ~F0 for the
+// write-through publish + F1 per other piece the last block reads back.
+// MAECLIP_GEMM_BM=256 / 192 forces a tile height, MAECLIP_GEMM_SK=0 / 1
+// disables / forces stream-K wherever the tiles leave a partial last round (A/B,
+// tests).
+struct TileChoice {
+  int bm;
+  SkPlan sk;
+};
+int64_t sk_workspace_bytes(int ncu) { return SK_CNT_BYTES + 2 * (int64_t)ncu * SK_SLOT; }
+
+TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
+  const char* eb = getenv("MAECLIP_GEMM_BM");
+  const int force_bm = (eb && *eb) ? atoi(eb) : 0;
+  const char* es = getenv("MAECLIP_GEMM_SK");
+  const int sk_mode = (es && *es) ? atoi(es) : 2;   // 0 off, 1 forced, 2 cost model
+  const bool plain = a.splitk <= 1 && a.batch == 1;
+  const bool allow192 = force_bm != 256 && plain && a.a_layout == LAY_KC && !a.colsum_partial;
+  const bool allow256 = force_bm != 192 || !allow192;
+  const bool allow_sk = plain && sk_mode != 0 && a.workspace != nullptr && ncu <= 256;
+  const int64_t gn = (a.N + 255) / 256, NT = a.K / KT;
+  constexpr double EPI_C = 2.5, F0 = 2.0, F1 = 2.0;
+  TileChoice best = {256, {0, 0, 0, nullptr, nullptr}};
+  double best_cost = 1e30;
+  for (int bm : {256, 192}) {
+    if ((bm == 256 && !allow256) || (bm == 192 && !allow192)) continue;
+    const double c = bm == 192 ? 0.89 : 1.0;
+    const int64_t T = (a.M + bm - 1) / bm * gn, full = T / ncu, R = T % ncu;
+    const double dp = (double)((T + ncu - 1) / ncu) * (NT * c + EPI_C);
+    if (dp < best_cost - 1e-9) {
+      best_cost = dp;
+      best = {bm, {0, 0, 0, nullptr, nullptr}};
+    }
+    if (!allow_sk || R == 0 || R * NT >= (1ll << 30)) continue;
+    const int64_t skw = (R * NT + ncu - 1) / ncu;
+    const int64_t np = std::min<int64_t>((NT + skw - 1) / skw + 1, R * NT);
+    const double cost = (full * NT + skw) * c + (full + 1) * EPI_C + (np > 1 ? F0 + F1 * (np - 1) : 0.0);
+    if (sk_mode == 1 || cost < best_cost - 1e-9) {
+      best_cost = sk_mode == 1 ? -1.0 : cost;
+      SkPlan p;
+      p.Tdp = (int)(full * ncu);
+      p.skw = (int)skw;
+      p.NT = (int)NT;
+      p.cnt = (unsigned*)a.workspace;
+      p.slots = (float*)((char*)a.workspace + SK_CNT_BYTES);
+      best = {bm, p};
+    }
+  }
+  return best;
+}
+
+template <typename KernT, typename ArgT>
+void launch_persistent(KernT kern, int lds, int64_t tiles, int ncu, bool sk, const ArgT& g, hipStream_t s) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  // one block per CU: persistent over tiles (stream-K: the whole grid, the
+  // block positions the plan was made for)
+  const int grid = sk ? ncu : (int)(tiles < ncu ? tiles : ncu);
+  hipLaunchKernelGGL(kern, dim3(grid, 1, 1), dim3(512), lds, s, g);
 }
 
 template <int LA, int LB, typename OutT, int EPI>
@@ -912,14 +1104,26 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   const int gn = (int)((a.N + 255) / 256);
   const int S = a.splitk > 1 ? a.splitk : 1;
   const int ncu = gemm4_ncu();
-  if constexpr (LA == LAY_KC) {
-    if (use_bm192(a, ncu)) {
-      auto kern = gemm4_kernel<LA, LB, OutT, EPI, false, 192>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_ALL);
-      const int tiles = (int)((a.M + 191) / 192) * gn;
-      hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_ALL, s, a);
-      MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
-      return 0;
+  Gemm4Args g = {};
+  g.a = a;
+  if (S == 1 && a.batch == 1) {
+    const TileChoice tc = choose_tiles(a, 64, ncu);
+    g.sk = tc.sk;
+    const bool sk = tc.sk.skw > 0;
+    if constexpr (LA == LAY_KC) {
+      if (tc.bm == 192) {
+        const int64_t tiles = (a.M + 191) / 192 * gn;
+        if (sk) launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192, true>, TileM<192>::LDS_ALL, tiles, ncu, true, g, s);
+        else launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
+        MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
+        return 0;
+      }
+      if (sk) {
+        launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 256, true>, TileM<256>::LDS_ALL, (a.M + 255) / 256 * gn,
+                          ncu, true, g, s);
+        MC_CHECK_LAUNCH("maeclip_gemm(v4, stream-K)");
+        return 0;
+      }
     }
   }
   const int gm = (int)((a.M + 255) / 256);
@@ -929,13 +1133,16 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   // split-K / batched launches get one block per (tile, slice, batch)
   const int tiles = gm * gn;
   const int grid = (S * a.batch > 1 || tiles < ncu) ? tiles : ncu;
-  hipLaunchKernelGGL(kern, dim3(grid, S, (unsigned)a.batch), dim3(512), TileM<256>::LDS_ALL, s, a);
+  hipLaunchKernelGGL(kern, dim3(grid, S, (unsigned)a.batch), dim3(512), TileM<256>::LDS_ALL, s, g);
   MC_CHECK_LAUNCH("maeclip_gemm(v4)");
   return 0;
 }
 
 template <int LA, int LB, typename OutT>
 int epi4(const maeclip_gemm_args& a, hipStream_t s) {
+#ifdef GEMM4_DEV_SUBSET   // register / ISA inspection builds only: one epilogue
+  return launch4<LA, LB, OutT, EPI_NONE>(a, s);
+#else
   switch (a.epilogue) {
     case EPI_NONE: return launch4<LA, LB, OutT, EPI_NONE>(a, s);
     case EPI_GELU: return launch4<LA, LB, OutT, EPI_GELU>(a, s);
@@ -944,6 +1151,7 @@ int epi4(const maeclip_gemm_args& a, hipStream_t s) {
     case EPI_MUL_AUX: return launch4<LA, LB, OutT, EPI_MUL_AUX>(a, s);
     default: return launch4<LA, LB, OutT, EPI_DGELU>(a, s);
   }
+#endif
 }
 
 template <int LA, int LB>
@@ -980,6 +1188,19 @@ bool gemm_v4_ok(const maeclip_gemm_args& a) {
   return true;
 }
 
+// scratch bytes of a stream-K launch of this shape (0: none chosen)
+int64_t gemm_v4_workspace(const maeclip_gemm_args& a) {
+  const bool f8 = a.dtype == MAECLIP_FP8_E4M3 || a.dtype == MAECLIP_FP8_E5M2;
+  if (f8 ? (a.K % 128 != 0 || a.M < 256 || a.N < 256) : !gemm_v4_ok(a)) return 0;
+  if (a.splitk > 1 || a.batch != 1) return 0;
+  if (!f8 && a.a_layout != LAY_KC) return 0;
+  maeclip_gemm_args b = a;
+  b.workspace = (float*)(uintptr_t)256;   // any non-null: "a workspace is offered"
+  const int ncu = gemm4_ncu();
+  return choose_tiles(b, f8 ? 128 : 64, ncu).sk.skw > 0 ? sk_workspace_bytes(ncu) : 0;
+}
+int64_t gemm_sk_counter_bytes() { return SK_CNT_BYTES; }
+
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
   if (a.a_layout == LAY_KC && a.b_layout == LAY_KC) return out4<LAY_KC, LAY_KC>(a, s);
   if (a.a_layout == LAY_KC && a.b_layout == LAY_RC) return out4<LAY_KC, LAY_RC>(a, s);
@@ -999,18 +1220,27 @@ namespace {
 template <typename OutT, int EPI, int F8>
 int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStream_t s) {
   const int ncu = gemm4_ncu();
-  Gemm8Args g;
+  Gemm4Args g = {};
   g.a = a;
   g.sa = sa;
   g.sb = sb;
   const int gn = (int)((a.N + 255) / 256);
-  if (use_bm192(a, ncu)) {
-    auto kern = gemm4_f8_kernel<OutT, EPI, F8, 192>;
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<192>::LDS_ALL);
-    const int tiles = (int)((a.M + 191) / 192) * gn;
-    hipLaunchKernelGGL(kern, dim3(tiles < ncu ? tiles : ncu, 1, 1), dim3(512), TileM<192>::LDS_ALL, s, g);
-    MC_CHECK_LAUNCH("maeclip_gemm_fp8(192-row tiles)");
-    return 0;
+  if (a.batch == 1) {
+    const TileChoice tc = choose_tiles(a, 128, ncu);
+    g.sk = tc.sk;
+    const bool sk = tc.sk.skw > 0;
+    const int64_t tiles = (a.M + tc.bm - 1) / tc.bm * gn;
+    if (tc.bm == 192) {
+      if (sk) launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 192, true>, TileM<192>::LDS_ALL, tiles, ncu, true, g, s);
+      else launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
+      MC_CHECK_LAUNCH("maeclip_gemm_fp8(192-row tiles)");
+      return 0;
+    }
+    if (sk) {
+      launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 256, true>, TileM<256>::LDS_ALL, tiles, ncu, true, g, s);
+      MC_CHECK_LAUNCH("maeclip_gemm_fp8(stream-K)");
+      return 0;
+    }
   }
   auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
@@ -1023,6 +1253,9 @@ int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipS
 
 template <typename OutT, int F8>
 int epi_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStream_t s) {
+#ifdef GEMM4_DEV_SUBSET
+  return launch_f8<OutT, EPI_NONE, F8>(a, sa, sb, s);
+#else
   switch (a.epilogue) {
     case EPI_NONE: return launch_f8<OutT, EPI_NONE, F8>(a, sa, sb, s);
     case EPI_GELU: return launch_f8<OutT, EPI_GELU, F8>(a, sa, sb, s);
@@ -1031,6 +1264,7 @@ int epi_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStre
     case EPI_MUL_AUX: return launch_f8<OutT, EPI_MUL_AUX, F8>(a, sa, sb, s);
     default: return launch_f8<OutT, EPI_DGELU, F8>(a, sa, sb, s);
   }
+#endif
 }
 
 }  // namespace
@@ -1060,10 +1294,12 @@ extern "C" int32_t maeclip_gemm_fp8(const maeclip_gemm_args* a, const float* sca
   const int64_t lim = 0x7fffffffLL;
   MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "maeclip_gemm_fp8: operand exceeds 2^31 bytes");
   hipStream_t s = (hipStream_t)stream;
-  // no-epilogue / residual-form launches at K > 512: the vendor library with
-  // outer-vector scales (gemm_lib.hip); every other epilogue below
+  // calibration only (MAECLIP_GEMM_LIB=1): the vendor library with
+  // outer-vector scales for the plain / residual forms (gemm_lib.hip)
   if (maeclip::gemm_lib_fp8_ok(*a)) {
-    const int rc = maeclip::gemm_lib(*a, s, scale_a, scale_b);
+    maeclip_gemm_args b = *a;
+    if (b.workspace) b.workspace = (float*)((char*)b.workspace + SK_CNT_BYTES);
+    const int rc = maeclip::gemm_lib(b, s, scale_a, scale_b);
     if (rc != 1) return rc;
   }
   const bool e5 = a->dtype == MAECLIP_FP8_E5M2;

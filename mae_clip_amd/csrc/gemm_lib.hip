@@ -74,10 +74,12 @@ LibState& state() {
   return s;
 }
 
-// MAECLIP_GEMM_LIB: 0 = off (v4 for every plain GEMM), 2 = bf16 outputs only
+// MAECLIP_GEMM_LIB: 0 = off (default: this library's kernels for every GEMM),
+// 1 = vendor for the plain / residual forms at K > 512, 2 = bf16 outputs only
+// (calibration A/B only)
 int lib_mode() {
   const char* e = getenv("MAECLIP_GEMM_LIB");
-  return (e && *e) ? atoi(e) : 1;
+  return (e && *e) ? atoi(e) : 0;
 }
 
 // MAECLIP_GEMM_LIB_TUNE=1: time the heuristic's candidates once per shape

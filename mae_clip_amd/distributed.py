@@ -44,18 +44,22 @@ def all_gather_rows(x, group=None):
 _CTRL = {}
 
 
-def control_group(group=None):
+def control_group(group=None, create=False):
     """A gloo group over the same ranks as `group`, for host-side control
     messages (batch-size checks): a collective on it moves CPU memory only, so
-    it never synchronises the host with the GPU stream. Created collectively
-    by DataParallel.__init__ (every rank constructs one); None for a group
-    that is already gloo."""
+    it never synchronises the host with the GPU stream. None for a group that
+    is already gloo, and for one whose control group was never created.
+
+    dist.new_group must be entered by EVERY rank of the default group, so the
+    group is only ever created eagerly (create=True), by DataParallel.__init__
+    over the whole world, where every rank constructs one; a subgroup gets
+    none (check_equal_rows then all-reduces on the group itself)."""
     key = group if group is not None else dist.group.WORLD
     if dist.get_backend(group) == "gloo":
         return None
-    if key not in _CTRL:
+    if key not in _CTRL and create:
         _CTRL[key] = dist.new_group(ranks=dist.get_process_group_ranks(key), backend="gloo")
-    return _CTRL[key]
+    return _CTRL.get(key)
 
 
 def check_equal_rows(n, group=None, device=None):
@@ -72,6 +76,8 @@ def check_equal_rows(n, group=None, device=None):
         return
     t = torch.tensor([n, -n], dtype=torch.int64)
     ctrl = control_group(group)
+    if ctrl is None and dist.get_backend(group) != "gloo" and device is not None:
+        t = t.to(device)   # no control group (a subgroup): the device group itself
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ctrl if ctrl is not None else group)
     hi, lo = int(t[0]), -int(t[1])
     if hi != lo:
@@ -177,7 +183,8 @@ class DataParallel:
         self.grad_dtype = grad_dtype
         self.world = dist.get_world_size(group)
         model.process_group = group if group is not None else dist.group.WORLD
-        control_group(group)   # collective: every rank creates the host control group here
+        if group is None or group == dist.group.WORLD:
+            control_group(group, create=True)   # collective over the world: every rank constructs a DataParallel
         self.params = [p for p in model.parameters() if p.requires_grad]
         if broadcast:
             with torch.no_grad():

@@ -51,16 +51,22 @@ def _call(name, *args):
 
 # ------------------------------------------------------------------ GEMM
 _SCRATCH = {}
+_SCRATCH_RETIRED = []
 
 
 def _stream_scratch(device, nbytes):
-    """Per-(device, stream) scratch kept for the process (the vendor library's
-    workspace of maeclip_gemm's plain GEMMs): launches on one stream run in
-    order and share it; a concurrently running stream gets its own."""
+    """Per-(device, stream) scratch kept for the process (maeclip_gemm's
+    stream-K counters and partial tiles): launches on one stream run in order
+    and share it; a concurrently running stream gets its own. Allocated zeroed
+    (the stream-K arrival counters at its start must be zero; every completed
+    launch leaves them zero). A buffer outgrown by a larger request is kept
+    alive, never freed: a captured HIP graph may still address it."""
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     t = _SCRATCH.get(key)
     if t is None or t.numel() * 4 < nbytes:
-        t = torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32)
+        if t is not None:
+            _SCRATCH_RETIRED.append(t)
+        t = torch.zeros((nbytes + 3) // 4, device=device, dtype=torch.float32)
         _SCRATCH[key] = t
     return t
 

@@ -66,6 +66,94 @@ def test_gemm_bm192(dev, b_lay, mnk, monkeypatch):
         assert err / scale < (2e-5 * math.sqrt(Kd) if out == torch.float32 else 1e-2), (out, err, scale)
 
 
+def _sk_counters_zero():
+    """every per-stream GEMM scratch: the stream-K arrival counters (its first
+    16 KiB) are back to zero after the launches completed"""
+    torch.cuda.synchronize()
+    for t in K._SCRATCH.values():
+        assert int(t[:4096].view(torch.int32).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("b_lay", [0, 1])
+@pytest.mark.parametrize("mnk", [(6400, 768, 3072), (6400, 2304, 768), (25216, 512, 2048), (50432, 512, 1536),
+                                 (1000, 520, 192), (300, 264, 640), (12800, 768, 768)])
+@pytest.mark.parametrize("mode", ["sk", "sk192", "auto"])
+def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
+    """Stream-K plain launches (the cut tiles summed in the same launch by the
+    block that arrives last, gemm4.hip sk_fixup): forced on every shape whose
+    tiles leave a partial last round ("sk"; "sk192" on 192-row tiles), or the
+    cost model's own choice ("auto"). Shapes: the micro-batch's encoder dgrads
+    (75 tiles for 256 CUs), the decoder's N = 512 dgrads (198 tiles; 394 =
+    one whole round + 138 stream-K tiles), tiny ragged launches where most
+    blocks get no K-tile and a tile is cut into up to 3 pieces of one K-tile.
+    vs fp64; bitwise equal on repeat (the summation order is fixed whichever
+    block arrives last); counters left zero."""
+    if mode != "auto":
+        monkeypatch.setenv("MAECLIP_GEMM_SK", "1")
+    if mode == "sk192":
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    M, N, Kd = mnk
+    A = _rand((M, Kd), torch.bfloat16, dev, seed=11)
+    B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, scale=0.5, seed=12)
+    ref = _ref_mm(A, B.t() if b_lay == 0 else B)
+    scale = ref.abs().max().item()
+    for out in (torch.float32, torch.bfloat16):
+        C = torch.empty((M, N), device=dev, dtype=out)
+        K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, 0, b_lay)
+        err = (C.double() - ref).abs().max().item()
+        assert err / scale < (2e-5 * math.sqrt(Kd) if out == torch.float32 else 1e-2), (out, err, scale)
+        C2 = torch.empty_like(C)
+        for _ in range(2):
+            K.gemm(A, B, C2, M, N, Kd, A.stride(0), B.stride(0), N, 0, b_lay)
+            assert torch.equal(C, C2)
+    _sk_counters_zero()
+
+
+@pytest.mark.parametrize("mode", ["sk", "sk192"])
+def test_gemm_stream_k_epilogues(dev, mode, monkeypatch):
+    """Every fused epilogue behind the stream-K fix-up (the last block runs it
+    on the summed tile): bias + GELU / GELU' (aux_out), fp32 residual, column
+    sums, dGELU, mul-aux + residual; M = 3000 x N = 768 (36 / 48 tiles, every
+    tile cut) at K = 1024."""
+    monkeypatch.setenv("MAECLIP_GEMM_SK", "1")
+    if mode == "sk192":
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    M, N, Kd = 3000, 768, 1024
+    x = _rand((M, Kd), torch.bfloat16, dev, seed=13)
+    w = _rand((N, Kd), torch.bfloat16, dev, scale=0.03, seed=14)
+    bias = _rand((N,), torch.float32, dev, seed=15)
+    resid = _rand((M, N), torch.float32, dev, seed=16)
+    ref = _ref_mm(x, w.t()) + bias.double()
+    tol = 4e-2
+    pre = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+    y = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU, aux_out=pre)
+    assert (pre.double() - ref).abs().max().item() < tol
+    assert (y.double() - torch.nn.functional.gelu(ref)).abs().max().item() < tol
+    y2 = K.linear_fwd(x, w, bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=resid)
+    assert (y2.double() - (ref + resid.double())).abs().max().item() < 1e-3
+    part = torch.empty((K.gemm_colsum_rows(M), N), device=dev, dtype=torch.float32)
+    y3 = K.linear_fwd(x, w, bias, out_dtype=torch.float32, colsum=part)
+    assert (K.colsum_reduce(part).double() - y3.double().sum(0)).abs().max().item() < 1e-2
+    d = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+    y4 = K.linear_fwd(x, w, bias, epilogue=K.EPI_GELU_D, aux_out=d)
+    r64 = ref.clone().requires_grad_(True)
+    gref = torch.autograd.grad(torch.nn.functional.gelu(r64).sum(), r64)[0]
+    assert (y4.double() - torch.nn.functional.gelu(ref)).abs().max().item() < tol
+    assert (d.double() - gref).abs().max().item() < tol
+    dy = _rand((M, N), torch.bfloat16, dev, seed=17)
+    aux = _rand((M, Kd), torch.bfloat16, dev, seed=18)
+    dx = K.linear_dgrad(dy, w, epilogue=K.EPI_DGELU, aux=aux, out_dtype=torch.float32)
+    a64 = aux.double().requires_grad_(True)
+    g = torch.autograd.grad(torch.nn.functional.gelu(a64).sum(), a64)[0]
+    ref_dx = _ref_mm(dy, w) * g
+    assert (dx.double() - ref_dx).abs().max().item() < 1e-3 * max(1.0, ref_dx.abs().max().item())
+    rd = _rand((M, Kd), torch.float32, dev, seed=19)
+    dx5 = K.linear_dgrad(dy, w, epilogue=K.EPI_MUL_AUX, aux=aux, out_dtype=torch.float32, resid=rd)
+    ref5 = _ref_mm(dy, w) * aux.double() + rd.double()
+    assert (dx5.double() - ref5).abs().max().item() < 1e-3 * max(1.0, ref5.abs().max().item())
+    _sk_counters_zero()
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M", [300, 700])   # fp32: 32x32-tile small kernel / 128x128 MFMA kernel
 @pytest.mark.parametrize("bm", ["auto", "192"])

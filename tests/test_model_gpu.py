@@ -633,10 +633,13 @@ def test_stack_microbatches_match_whole_batch(dev, monkeypatch):
     column partials are summed in another grouping, within 1e-5 relative L2.
     C2 model shapes at B = 128, so both micro-batches keep whole 64-row
     groups (encoder 64 x 50 rows, decoder 64 x 197). The library's own GEMM
-    kernels throughout (MAECLIP_GEMM_LIB=0): the vendor library may pick another
-    algorithm for another row count, so its plain GEMMs are equal only to
-    rounding (test_gemm_vendor_plain)."""
+    kernels throughout, stream-K off (MAECLIP_GEMM_SK=0): a stream-K launch
+    cuts its tiles' K ranges at points that depend on the row count, so the
+    micro-batch and whole-batch GEMMs would agree only to rounding
+    (test_gemm_stream_k checks stream-K itself; the captured micro-batched
+    step with the default settings: test_captured_step_matches_eager_microbatched)."""
     monkeypatch.setenv("MAECLIP_GEMM_LIB", "0")
+    monkeypatch.setenv("MAECLIP_GEMM_SK", "0")
     from tests.helpers import product_config
     from mae_clip_amd.CLIP import CLIPModel
     from mae_clip_amd import functions as Fn
@@ -665,3 +668,44 @@ def test_stack_microbatches_match_whole_batch(dev, monkeypatch):
             worst = max(worst, e)
             assert e < 1e-5, (n, e)
     record_parity("stack_microbatches_2_vs_1", worst_bias_ln_grad_relL2=worst)
+
+
+def test_captured_step_matches_eager_microbatched(dev):
+    """The production combination, default settings: C2 model shapes at B = 128,
+    where every bf16 stack runs as two micro-batch chains on two streams
+    (encoder 64 x 50, decoder 64 x 197, text 64 x 25 rows per chain), the
+    default GEMM path (stream-K where the cost model picks it), train mode
+    (step-keyed MAE and dropout masks), side stream on. CapturedStep (two eager
+    steps, the third captured as one HIP graph with the chains' fork / join
+    inside it, then replays) == eager steps: the same losses, bitwise-equal
+    final weights and the same MAE masks."""
+    from tests.helpers import product_config
+    from mae_clip_amd.CLIP import CLIPModel
+    from mae_clip_amd.optim import AdamW
+    from mae_clip_amd.graph import CapturedStep
+    from mae_clip_amd import functions as Fn
+    runs = []
+    for captured in (False, True):
+        with product_config(precision="bf16", **VITB_C2):
+            torch.manual_seed(0)
+            m = CLIPModel().to(dev).train()
+            assert Fn.microbatch_count(Fn.StackSpec(B=128, n=50, D=768, H=12, eps=1e-6, dtype=torch.bfloat16,
+                                                    wT=[])) == 2
+            assert Fn.microbatch_count(Fn.StackSpec(B=128, n=197, D=512, H=16, eps=1e-6, dtype=torch.bfloat16,
+                                                    wT=[])) == 2
+        opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
+        runner = CapturedStep(m, opt, enabled=captured)
+        losses, masks = [], []
+        for it in range(5):
+            batch = {k: v.to(dev) for k, v in make_batch(128, 224, seed=40 + it).items()}
+            losses.append(runner.step(batch).item())
+            masks.append(m.last_mask[2].clone())
+        runs.append((losses, masks, m, runner))
+    (le, ke, me, _), (lg, kg, mg, rg) = runs
+    assert rg.captures == 1
+    assert le == lg, (le, lg)
+    assert len(set(le)) == len(le)
+    for a, b in zip(ke, kg):
+        assert torch.equal(a, b)
+    for (n1, p1), (n2, p2) in zip(me.named_parameters(), mg.named_parameters()):
+        assert torch.equal(p1, p2), n1

@@ -99,6 +99,9 @@ for s in $STEPS; do
     plainprobe) # per-shape own vs vendor plain GEMMs (tools/plain_gemm_probe.py)
       timeout -k 10 400 python -u tools/plain_gemm_probe.py > gpurun_out/plainprobe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/plainprobe_${TAG}.jsonl; exit 1; }
       cat gpurun_out/plainprobe_${TAG}.jsonl ;;
+    ownprobe) # per-shape own (stream-K) vs own data-parallel vs vendor (tools/own_vs_vendor_probe.py)
+      timeout -k 10 500 python -u tools/own_vs_vendor_probe.py > gpurun_out/ownprobe_${TAG}.jsonl 2>&1 || { tail -30 gpurun_out/ownprobe_${TAG}.jsonl; exit 1; }
+      cat gpurun_out/ownprobe_${TAG}.jsonl ;;
     cfgs)    # C1 / C4 bf16 / C4 fp8 bench lines (tools/cfg_runs.sh)
       TAG=$TAG timeout -k 10 1100 bash tools/cfg_runs.sh > gpurun_out/cfgs_${TAG}.txt 2>&1 || { tail -30 gpurun_out/cfgs_${TAG}.txt; exit 1; }
       cat gpurun_out/cfgs_${TAG}.txt ;;
