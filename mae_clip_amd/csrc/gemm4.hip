@@ -522,11 +522,13 @@ __device__ __forceinline__ bool sk_fixup(v4f (&acc)[NF][4], const SkPlan& sk, co
   bool last = *flag == 1;
   if (!last) {
     const int so = skp * 2 * (int)SK_SLOT + (u.slot & 1) * (int)SK_SLOT;
+#ifndef SKX_NO_PUBLISH   // diagnostic builds only: time without the partial stores
 #pragma unroll
     for (int i = 0; i < NF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rs, vo + (i * 4 + j) * 1024, so, 16);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SEG_BARRIER();
     if (tid == 0)
@@ -1163,6 +1165,11 @@ int out4(const maeclip_gemm_args& a, hipStream_t s) {
 
 #ifdef GEMM4_STAMPS
 extern "C" int maeclip_debug_gemm4_stamps(uint64_t* host, int n) {
+  // n < 0: zero the stamp buffer (host unused)
+  if (n < 0) {
+    static uint64_t zero[256 * 8 * 2 * 4] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+  }
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(uint64_t) * (size_t)n) == hipSuccess ? 0 : -1;
 }
 #endif

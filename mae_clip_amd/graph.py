@@ -32,6 +32,8 @@ from __future__ import annotations
 
 import torch
 
+from . import kernels as K
+
 
 class CapturedStep:
     def __init__(self, model, optimizer, enabled: bool = True, eager_steps: int = 1, dp=None):
@@ -148,13 +150,19 @@ class CapturedStep:
         # backward seed allocated outside the graph: loss.backward() would fill
         # a fresh ones tensor inside every replay
         one = torch.ones((), device=next(self.model.parameters()).device, dtype=torch.float32)
+        replay = torch.cuda.current_stream().cuda_stream
         with torch.cuda.graph(g, capture_error_mode="relaxed"):
-            loss = self.model(self.static)
-            torch.autograd.backward(loss, grad_tensors=one.expand_as(loss) if loss.dim() else one)
-            if self.dp is not None:
-                self.dp.sync_gradients()
-            self.opt.step()
-            self._publish(loss)
+            cap = torch.cuda.current_stream().cuda_stream
+            K.alias_stream(cap, replay)
+            try:
+                loss = self.model(self.static)
+                torch.autograd.backward(loss, grad_tensors=one.expand_as(loss) if loss.dim() else one)
+                if self.dp is not None:
+                    self.dp.sync_gradients()
+                self.opt.step()
+                self._publish(loss)
+            finally:
+                K.alias_stream(cap, None)
         # capture recorded the work without running it: undo its host-side counting
         self.model.step = model_step
         self.opt._advance_host_steps(-1)

@@ -52,6 +52,19 @@ def _call(name, *args):
 # ------------------------------------------------------------------ GEMM
 _SCRATCH = {}
 _SCRATCH_RETIRED = []
+_STREAM_ALIAS = {}   # capture stream -> the stream its graph is replayed on
+
+
+def alias_stream(capture_stream, replay_stream):
+    """While a graph is captured on `capture_stream` (torch.cuda.graph's own
+    stream), its GEMMs use the scratch of `replay_stream`, the stream the graph
+    is later replayed on: eager launches and replays are ordered on it, so they
+    can share one buffer, and the capture allocates (and zero-fills inside the
+    graph) nothing. `replay_stream=None` removes the alias."""
+    if replay_stream is None:
+        _STREAM_ALIAS.pop(capture_stream, None)
+    else:
+        _STREAM_ALIAS[capture_stream] = replay_stream
 
 
 def _stream_scratch(device, nbytes):
@@ -61,7 +74,8 @@ def _stream_scratch(device, nbytes):
     (the stream-K arrival counters at its start must be zero; every completed
     launch leaves them zero). A buffer outgrown by a larger request is kept
     alive, never freed: a captured HIP graph may still address it."""
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    s = torch.cuda.current_stream(device).cuda_stream
+    key = (device.index, _STREAM_ALIAS.get(s, s))
     t = _SCRATCH.get(key)
     if t is None or t.numel() * 4 < nbytes:
         if t is not None:
