@@ -13,7 +13,7 @@ build/obj/%.o: mae_clip_amd/csrc/%.hip mae_clip_amd/csrc/common.h include/maecli
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@ -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@
 
 clean:
 	rm -rf build $(LIB)

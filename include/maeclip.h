@@ -124,9 +124,8 @@ int64_t maeclip_gemm_colsum_rows(int64_t M);
 /* scratch bytes maeclip_gemm may use for *args when args->splitk <= 1 (pass
  * them as args->workspace; a NULL workspace is always valid, just slower) */
 int64_t maeclip_gemm_workspace(const maeclip_gemm_args* args);
-/* which implementation maeclip_gemm runs for *args: 0 = this library's
- * kernels, 1 = the vendor library (hipBLASLt: no-epilogue bf16 C or the fp32
- * residual form, bias allowed, K > 512; MAECLIP_GEMM_LIB=0 turns it off) */
+/* which implementation maeclip_gemm runs for *args: always 0 = this library's
+ * kernels (kept from ABI v9; the round-4 vendor-library path was removed) */
 int32_t maeclip_gemm_impl(const maeclip_gemm_args* args);
 int32_t maeclip_gemm_splitk(int64_t M, int64_t N, int64_t K);
 

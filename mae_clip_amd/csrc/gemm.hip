@@ -32,12 +32,7 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
-bool gemm_lib_ok(const maeclip_gemm_args& a);
-int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a = nullptr, const float* scale_b = nullptr);
-int64_t gemm_lib_workspace(const maeclip_gemm_args& a);
-bool gemm_lib_fp8_ok(const maeclip_gemm_args& a);
 int64_t gemm_v4_workspace(const maeclip_gemm_args& a);
-int64_t gemm_sk_counter_bytes();
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_small_ok(const maeclip_gemm_args& a);
 int64_t gemm_small_workspace(const maeclip_gemm_args& a);
@@ -432,18 +427,10 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   // splitk_reduce (v1's launch() reduces by itself)
   if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small(*a, s);
   int rc = 1;
-  // calibration only (MAECLIP_GEMM_LIB=1, off by default): the vendor library
-  // for the plain / residual forms; its workspace starts past the stream-K
-  // counters, which must stay zero
-  if (forced == 0 && maeclip::gemm_lib_ok(*a)) {
-    maeclip_gemm_args b = *a;
-    if (b.workspace) b.workspace = (float*)((char*)b.workspace + maeclip::gemm_sk_counter_bytes());
-    rc = maeclip::gemm_lib(b, s);
-    if (rc != 1) return rc;
-  }
-  // v4 (8-wave ping-pong 256x256, persistent, buffer-descriptor DMA, stream-K
-  // when the tiles leave a partial last round) wherever its shape conditions
-  // hold; MAECLIP_GEMM_VARIANT=1..7 pins a v2 tile, 99 v1
+  // v4 (8-wave ping-pong 256x256 / 192x256, persistent, buffer-descriptor DMA,
+  // split tiles with an in-launch fix-up when the tiles leave most of the grid
+  // idle) wherever its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a
+  // v2 tile, 99 v1
   if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
     rc = maeclip::gemm_v4(*a, s);
   else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
@@ -457,24 +444,23 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
 
 extern "C" int64_t maeclip_gemm_colsum_rows(int64_t M) { return (M + 63) / 64; }
 
+// Every GEMM runs on this library's kernels (ABI v9 kept the query; the
+// round-4 vendor path was removed in round 5).
 extern "C" int32_t maeclip_gemm_impl(const maeclip_gemm_args* a) {
-  if (!a) return 0;
-  static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
-  if (forced == 99 || maeclip::gemm_small_ok(*a)) return 0;
-  return (forced == 0 && (maeclip::gemm_lib_ok(*a) || maeclip::gemm_lib_fp8_ok(*a))) ? 1 : 0;
+  (void)a;
+  return 0;
 }
 
 // Scratch bytes maeclip_gemm may use for this call when the caller asks for no
 // split-K itself (splitk <= 1): the small-fp32 path's K-slice partials, or the
-// vendor library's workspace for plain bf16 GEMMs (one workspace per stream).
+// v4 split plan's arrival counters + fp32 partial tiles (one workspace per
+// stream: launches on one stream run in order; the counters must be zero
+// before the first launch, and every completed launch leaves them zero).
 extern "C" int64_t maeclip_gemm_workspace(const maeclip_gemm_args* a) {
   if (!a || a->splitk > 1) return 0;
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
   if (forced != 99 && maeclip::gemm_small_ok(*a)) return maeclip::gemm_small_workspace(*a);
-  int64_t ws = (forced == 0 || forced == 8) ? maeclip::gemm_v4_workspace(*a) : 0;
-  if (forced == 0 && maeclip::gemm_lib_workspace(*a) > 0)
-    ws = std::max(ws, maeclip::gemm_sk_counter_bytes() + maeclip::gemm_lib_workspace(*a));
-  return ws;
+  return (forced == 0 || forced == 8) ? maeclip::gemm_v4_workspace(*a) : 0;
 }
 
 // Slice count for split-K (the wgrad shapes of the hot path have only 4-36

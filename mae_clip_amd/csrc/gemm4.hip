@@ -467,24 +467,36 @@ struct Unit4 {
   int tl;             // stream-K: remainder tile index
 };
 
-// Stream-K plan of a plain launch (maeclip_gemm with a workspace): tiles
-// [0, Tdp) run whole on the persistent grid (Tdp a multiple of it); the
-// K-tiles of the R = T - Tdp remainder tiles are dealt out skw per block in
-// XCD-contiguous block-position order, so every block does the same work and
-// a launch with fewer tiles than CUs still fills the chip (the micro-batch's
-// 6400-row encoder shapes: 75 tiles of 256 x 256 for 256 CUs). A block's
-// range cuts at most two tiles: its first and its last. The pieces of a cut
-// tile are summed IN THE SAME LAUNCH by the block that arrives last
-// (sk_fixup): no second launch, no waiting, a fixed summation order.
+// Split plan of a plain launch (maeclip_gemm with a workspace): every tile's
+// K range is cut into S slices, one unit per (tile, slice), units tile-major
+// and dealt out in XCD-contiguous chunks of the persistent grid, so a launch
+// with fewer tiles than CUs still fills the chip (the micro-batch's 6400-row
+// encoder shapes: 75 tiles of 256 x 256 for 256 CUs) and the blocks on one XCD
+// work the same K-range of neighbouring tiles at the same time, sharing A rows
+// / B columns in its L2. (Stream-K ranges -- every block an equal run of
+// K-tiles across tile boundaries -- start every block at a different K and
+// lose that reuse: 2.5x the K-tile time, profiles/r05/stream_k_diag_r5c.jsonl;
+// removed.) The slices of a tile are summed IN THE SAME LAUNCH by the block
+// that arrives last (sk_fixup): no second launch, no waiting, a fixed
+// summation order. Slice 0 is the longest, by `lead` K-tiles per other slice
+// (L0 = ceil((NT + (S - 1) lead) / S), the rest split evenly): the other
+// slices finish first and publish while slice 0 still computes, so slice 0
+// usually finds them all published and sums without publishing its own.
 // Workspace: [SK_CNT_BYTES] arrival counters (zero before the first launch,
-// left zero by every completed launch), then 2 slots of SK_SLOT bytes per block.
+// left zero by every completed launch), then one SK_SLOT partial per unit
+// (slot t * S + s), at most 2 per CU.
 constexpr int SK_CNT_STRIDE = 16;                 // counter words apart (64 B)
 constexpr int64_t SK_CNT_BYTES = 256 * SK_CNT_STRIDE * 4;
 constexpr int64_t SK_SLOT = 256 * 256 * 4;        // one fp32 256x256 tile
+constexpr int SPLIT_MAX = 2;   // the fix-up sums two partials
 struct SkPlan {
-  int Tdp, skw, NT;   // skw = 0: no stream-K
+  int NT;             // K-tiles of the whole K
+  int S;              // slices per tile (0: no split)
+  int L0;             // K-tiles of slice 0 (the others share NT - L0)
+  int nsl;            // fp32 256x256 slots in the workspace
   unsigned* cnt;
   float* slots;
+  __host__ __device__ bool on() const { return S > 0; }
 };
 struct Gemm4Args {
   maeclip_gemm_args a;
@@ -493,41 +505,41 @@ struct Gemm4Args {
   const float* sb;
 };
 
-// Fix-up of one cut tile (stream-K piece `piece` of `np`): returns true in the
-// block that arrives last, whose acc then holds the whole tile's sum and which
-// runs the epilogue. Hand-off (MI355X_MICROARCH.md, valid forms, first row of
-// the sc1 table): every piece is stored write-through (16-B sc1 stores), each
-// storing wave drains with vmcnt(0), a workgroup barrier, then ONE lane adds to
-// the tile's agent-scope counter; the block whose add returns np - 1 (or whose
-// sc1 poll already reads np - 1 and so skips its own store) reads the other
-// pieces with sc1 loads only. The summation order is fixed by piece index
-// whichever block reduces: ((p0 + p1) + p2) + ..., the reducer's own partial
-// entering at its position, so the output bits do not depend on arrival order.
-// Slot layout is fragment-native (the accumulator registers as they stand, 1
-// KiB per wave-instruction): [wave][row fragment][col fragment][lane] x 16 B.
+// Fix-up of one split tile (slice u.slot of S = 2): returns true in the block
+// that arrives last, whose acc then holds the whole tile's sum and which runs
+// the epilogue. Hand-off (MI355X_MICROARCH.md, publish-large / handoff-payload):
+// every slice but the last to arrive is stored write-through (16-B sc1
+// stores), each storing wave drains with vmcnt(0), a workgroup barrier, then
+// ONE lane adds to the tile's agent-scope counter; the block whose add returns
+// S - 1 (or whose poll already reads S - 1 and so skips its own store: slice
+// 0, by its lead) reads the other slices with sc1 loads only. The summation
+// order is fixed by slice index whichever block reduces: ((p0 + p1) + p2),
+// the reducer's own partial entering at its position, so the output bits do
+// not depend on arrival order (p0 + p1 == p1 + p0). Slot layout is fragment-native (the accumulator
+// registers as they stand, 1 KiB per wave-instruction): [wave][row
+// fragment][col fragment][lane] x 16 B.
 template <int NF>
-__device__ __forceinline__ bool sk_fixup(v4f (&acc)[NF][4], const SkPlan& sk, const Unit4& u, int skp, int G,
-                                         int* flag, int tid, int wave, int lane) {
-  // pieces p_first .. p_last (block positions) of remainder tile u.tl
-  const int NT = sk.NT, w = sk.skw;
-  const int p_first = u.tl * NT / w, np = ((u.tl + 1) * NT - 1) / w - p_first + 1;
+__device__ __forceinline__ bool sk_fixup(v4f (&acc)[NF][4], const SkPlan& sk, const Unit4& u, int* flag, int tid,
+                                         int wave, int lane) {
+  const int np = sk.S, r = u.slot;
   unsigned* cnt = sk.cnt + u.tl * SK_CNT_STRIDE;
   const unsigned last_count = (unsigned)(np - 1);
-  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sk.slots, (short)0, (int)(2 * (int64_t)G * SK_SLOT),
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sk.slots, (short)0, (int)((int64_t)sk.nsl * SK_SLOT),
                                                       0x00020000);
   const int vo = lane * 16 + wave * NF * 4 * 1024;
+  const int sbase = u.tl * np * (int)SK_SLOT;
   if (tid == 0) *flag = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last_count ? 1 : 0;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   SEG_BARRIER();
   bool last = *flag == 1;
   if (!last) {
-    const int so = skp * 2 * (int)SK_SLOT + (u.slot & 1) * (int)SK_SLOT;
 #ifndef SKX_NO_PUBLISH   // diagnostic builds only: time without the partial stores
+    const int so = sbase + r * (int)SK_SLOT;
 #pragma unroll
     for (int i = 0; i < NF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rs, vo + (i * 4 + j) * 1024, so, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[i][j]), rs, vo, so + (i * 4 + j) * 1024, 16);
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SEG_BARRIER();
@@ -538,42 +550,30 @@ __device__ __forceinline__ bool sk_fixup(v4f (&acc)[NF][4], const SkPlan& sk, co
     last = *flag == 1;
   }
   if (!last) return false;
-  // the pieces' slots: piece p is held by block position bp = p_first + p, in
-  // its first (slot 0) or last (slot 1) job
-  auto slot_off = [&](int p) {
-    const int bp = p_first + p;
-    return bp * 2 * (int)SK_SLOT + ((int)((int64_t)bp * w / NT) == u.tl ? 0 : (int)SK_SLOT);
-  };
-  const int r = skp - p_first;
 #ifndef SKX_NO_REDUCE
-  // one row fragment (4 accumulators) at a time: (p_0 + ... + p_{r-1}) + own,
-  // then + p_{r+1} + ... in order
   auto ld4 = [&](int p, int i, v4f (&L)[4]) {
-    const int so = slot_off(p);
+    const int so = sbase + p * (int)SK_SLOT;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      L[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + (i * 4 + j) * 1024, so, 16));
+      L[j] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so + (i * 4 + j) * 1024, 16));
   };
+  // (the per-fragment offset rides in the scalar soffset: as a per-lane
+  // voffset it would take one VGPR per fragment, past the immediate's range)
+  // S = 2: the other slice's two row fragments at a time, 8 16-B loads per
+  // lane in flight (the hand-off read is latency-bound below that)
+  const int o = 1 - r;
 #pragma unroll
-  for (int i = 0; i < NF; ++i) {
-    if (r > 0) {
-      v4f T[4];
-      ld4(0, i, T);
-      for (int p = 1; p < r; ++p) {
-        v4f L[4];
-        ld4(p, i, L);
+  for (int i = 0; i < NF; i += 2) {
+    v4f L[2][4];
+    ld4(o, i, L[0]);
+    ld4(o, i + 1, L[1]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) T[j] += L[j];
-      }
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = T[j] + acc[i][j];
-    }
-    for (int p = r + 1; p < np; ++p) {
-      v4f L[4];
-      ld4(p, i, L);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] += L[j];
-    }
+      for (int j = 0; j < 4; ++j) acc[i + ii][j] += L[ii][j];   // p0 + p1 == p1 + p0
+    // keep the next fragments' loads below this sum: hoisted, they would
+    // hold the whole partial beside acc
+    __builtin_amdgcn_sched_barrier(0);
   }
 #endif
   if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -640,8 +640,8 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     const int S = SPLIT ? args.splitk : 1;
     klen = (((int)args.K + S - 1) / S + KT - 1) / KT * KT;
   }
-  // stream-K remainder (grouped: gp; plain launches: *skp_): tiles [Tdp, Ttot)
-  // are dealt out by K-tiles, skw per block
+  // stream-K remainder (grouped launches: gp): tiles [Tdp, Ttot) are dealt out
+  // by K-tiles, skw per block
   int Ttot = T, Tdp = T, skw = 0, NTr = 1;
   if (GRP && gp->skw > 0) {
     Ttot = gp->T;
@@ -649,10 +649,10 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     skw = gp->skw;
     NTr = gp->NT;
   }
+  int skS = 0;   // aligned split: units = (tile, slice)
   if (SK) {
-    Tdp = T = skp_->Tdp;
-    skw = skp_->skw;
-    NTr = skp_->NT;
+    skS = skp_->S;
+    Ttot = Tdp = T = T * skS;
   }
   auto unit = [&](int u) {
     Unit4 w;
@@ -681,15 +681,26 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       w.M = (int)args.M;
       w.N = (int)args.N;
       w.K = (int)args.K;
-      w.m0 = (u / gn) * BM;
-      w.n0 = (u % gn) * 256;
-      w.slice = blockIdx.y;
+      const int tile = skS > 0 ? u / skS : u;
+      w.m0 = (tile / gn) * BM;
+      w.n0 = (tile % gn) * 256;
+      w.slice = skS > 0 ? u - tile * skS : (int)blockIdx.y;
       w.prob = 0;
     }
-    w.kbeg = w.slice * klen;
-    const int kend = min(w.K, w.kbeg + klen);
-    w.nt = kend > w.kbeg ? (kend - w.kbeg) / KT : 0;
-    w.slot = -1;
+    if (SK && skS > 0) {
+      // slice 0: K-tiles [0, L0); slice s >= 1: its share of the rest
+      const int L0 = skp_->L0, rem = skp_->NT - L0, q = rem / (skS - 1), rr = rem % (skS - 1);
+      const int s1 = w.slice - 1;
+      const int kb = w.slice == 0 ? 0 : L0 + s1 * q + min(s1, rr);
+      w.nt = w.slice == 0 ? L0 : q + (s1 < rr ? 1 : 0);
+      w.kbeg = kb * KT;
+    } else {
+      w.kbeg = w.slice * klen;
+      const int kend = min(w.K, w.kbeg + klen);
+      w.nt = kend > w.kbeg ? (kend - w.kbeg) / KT : 0;
+    }
+    w.slot = skS > 0 ? w.slice : -1;   // aligned split: every unit is a piece
+    w.tl = skS > 0 ? u / skS : 0;
     return w;
   };
 
@@ -722,11 +733,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     }
   }
   auto job = [&](int j) -> Unit4 {
-    if (j < ndp) {
-      Unit4 w = unit(cbeg + li + j * nbx);
-      w.tl = 0;
-      return w;
-    }
+    if (j < ndp) return unit(cbeg + li + j * nbx);
     const int s = j - ndp, NT = NTr;
     const int tl = sk_t0 + s;
     const int k0 = s == 0 ? sk_k0 : 0;
@@ -927,7 +934,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
     // (the prologue fills buffer 0 and the other three halves of buffer 1)
     bool run_epi = true;
     if (SK && u.slot >= 0)
-      run_epi = sk_fixup<2 * MI>(acc, *skp_, u, skp, G, (int*)(smem + TM::BUF_T + TM::HALF_A), tid, wave, lane);
+      run_epi = sk_fixup<2 * MI>(acc, *skp_, u, (int*)(smem + TM::BUF_T + TM::HALF_A), tid, wave, lane);
     if (!run_epi) {
     } else if constexpr (BM != 256) {
       epilogue4<OutT, EPI, F8 != 0, BM>(args, acc, z, m0, n0, wm, wn, lane, scr, sa, sb);
@@ -1038,14 +1045,14 @@ int gemm4_ncu() {
   return cap > 0 && cap < ncu ? cap : ncu;
 }
 
-// Tile height and stream-K plan of a plain launch (one batch, no split-K),
-// from a cost model in units of one 256-row K-tile (~2.9k cycles, 64 KiB of
-// operand DMA per CU): a 192-row K-tile costs 0.89 of it (measured, encoder fc2
-// fwd, one round each); a tile's epilogue ~EPI_C; a stream-K fix-up ~F0 for the
-// write-through publish + F1 per other piece the last block reads back.
-// MAECLIP_GEMM_BM=256 / 192 forces a tile height, MAECLIP_GEMM_SK=0 / 1
-// disables / forces stream-K wherever the tiles leave a partial last round (A/B,
-// tests).
+// Tile height and split plan of a plain launch (one batch, no caller
+// split-K), from a cost model in units of one 256-row K-tile (~2.9k cycles, 64
+// KiB of operand DMA per CU): a 192-row K-tile costs 0.89 of it (measured,
+// encoder fc2 fwd, one round each); a tile's epilogue ~EPI_C; a split costs
+// slice 0's K-tiles (its lead hides the others' publish) + F1 per other slice
+// the last block reads back. MAECLIP_GEMM_BM=256 / 192 forces a tile height;
+// MAECLIP_GEMM_SK=0 disables the split; MAECLIP_GEMM_SPLIT=S forces a split
+// of S wherever it fits (A/B, tests).
 struct TileChoice {
   int bm;
   SkPlan sk;
@@ -1056,37 +1063,61 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
   const char* eb = getenv("MAECLIP_GEMM_BM");
   const int force_bm = (eb && *eb) ? atoi(eb) : 0;
   const char* es = getenv("MAECLIP_GEMM_SK");
-  const int sk_mode = (es && *es) ? atoi(es) : 2;   // 0 off, 1 forced, 2 cost model
+  const int sk_mode = (es && *es) ? atoi(es) : 1;   // 0 off, 1 cost model
+  const char* esp = getenv("MAECLIP_GEMM_SPLIT");
+  const int force_split = (esp && *esp) ? atoi(esp) : 0;
+  // the cost model's split only at K >= MAECLIP_GEMM_SPLIT_MINK (step A/B)
+  const char* emk = getenv("MAECLIP_GEMM_SPLIT_MINK");
+  const int64_t split_min_k = (emk && *emk) ? atoll(emk) : 0;
   const bool plain = a.splitk <= 1 && a.batch == 1;
   const bool allow192 = force_bm != 256 && plain && a.a_layout == LAY_KC && !a.colsum_partial;
   const bool allow256 = force_bm != 192 || !allow192;
   const bool allow_sk = plain && sk_mode != 0 && a.workspace != nullptr && ncu <= 256;
   const int64_t gn = (a.N + 255) / 256, NT = a.K / KT;
-  constexpr double EPI_C = 2.5, F0 = 2.0, F1 = 2.0;
-  TileChoice best = {256, {0, 0, 0, nullptr, nullptr}};
+  constexpr double EPI_C = 2.5, F1 = 2.0;
+  const SkPlan none = {0, 0, 0, 0, nullptr, nullptr};
+  // slice 0's lead per other slice (aligned split): about one publish of a
+  // 256 x 256 fp32 partial; MAECLIP_GEMM_SPLIT_D overrides
+  const char* ed = getenv("MAECLIP_GEMM_SPLIT_D");
+  const int lead = (ed && *ed) ? atoi(ed) : 4;
+  TileChoice best = {256, none};
   double best_cost = 1e30;
+  auto l0 = [&](int S) {
+    // slice 0 longer by `lead` per other slice, every other slice >= 1 K-tile
+    const int64_t L0 = (NT + (int64_t)(S - 1) * lead + S - 1) / S;
+    return (int)std::max<int64_t>(std::min<int64_t>(L0, NT - (S - 1)), (NT + S - 1) / S);
+  };
+  auto plan = [&](int S) {
+    SkPlan p = none;
+    p.NT = (int)NT;
+    p.S = S;
+    p.L0 = l0(S);
+    p.nsl = 2 * ncu;
+    p.cnt = (unsigned*)a.workspace;
+    p.slots = (float*)((char*)a.workspace + SK_CNT_BYTES);
+    return p;
+  };
   for (int bm : {256, 192}) {
     if ((bm == 256 && !allow256) || (bm == 192 && !allow192)) continue;
     const double c = bm == 192 ? 0.89 : 1.0;
-    const int64_t T = (a.M + bm - 1) / bm * gn, full = T / ncu, R = T % ncu;
+    const int64_t T = (a.M + bm - 1) / bm * gn, R = T % ncu;
     const double dp = (double)((T + ncu - 1) / ncu) * (NT * c + EPI_C);
-    if (dp < best_cost - 1e-9) {
+    if (dp < best_cost - 1e-9 && force_split == 0) {
       best_cost = dp;
-      best = {bm, {0, 0, 0, nullptr, nullptr}};
+      best = {bm, none};
     }
-    if (!allow_sk || R == 0 || R * NT >= (1ll << 30)) continue;
-    const int64_t skw = (R * NT + ncu - 1) / ncu;
-    const int64_t np = std::min<int64_t>((NT + skw - 1) / skw + 1, R * NT);
-    const double cost = (full * NT + skw) * c + (full + 1) * EPI_C + (np > 1 ? F0 + F1 * (np - 1) : 0.0);
-    if (sk_mode == 1 || cost < best_cost - 1e-9) {
-      best_cost = sk_mode == 1 ? -1.0 : cost;
-      SkPlan p;
-      p.Tdp = (int)(full * ncu);
-      p.skw = (int)skw;
-      p.NT = (int)NT;
-      p.cnt = (unsigned*)a.workspace;
-      p.slots = (float*)((char*)a.workspace + SK_CNT_BYTES);
-      best = {bm, p};
+    // split: 192-row tiles only (the 256-row body has no registers left for
+    // the fix-up: its split instantiation spilled inside the K loop)
+    if (!allow_sk || bm != 192 || (force_split == 0 && (R == 0 || a.K < split_min_k))) continue;
+    for (int S = 2; S <= SPLIT_MAX; ++S) {
+      if ((force_split > 0 && S != force_split) || T * S > 2 * ncu || T > 256 || NT < 2 * S) continue;
+      const int64_t rounds = (T * S + ncu - 1) / ncu;
+      // the publish of slices >= 1 runs while slice 0 computes its lead
+      const double cost = (double)rounds * l0(S) * c + EPI_C + F1 * (S - 1);
+      if (force_split > 0 || cost < best_cost - 1e-9) {
+        best_cost = force_split > 0 ? -1.0 : cost;
+        best = {bm, plan(S)};
+      }
     }
   }
   return best;
@@ -1111,19 +1142,13 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   if (S == 1 && a.batch == 1) {
     const TileChoice tc = choose_tiles(a, 64, ncu);
     g.sk = tc.sk;
-    const bool sk = tc.sk.skw > 0;
+    const bool sk = tc.sk.on();
     if constexpr (LA == LAY_KC) {
       if (tc.bm == 192) {
         const int64_t tiles = (a.M + 191) / 192 * gn;
         if (sk) launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192, true>, TileM<192>::LDS_ALL, tiles, ncu, true, g, s);
         else launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
         MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
-        return 0;
-      }
-      if (sk) {
-        launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 256, true>, TileM<256>::LDS_ALL, (a.M + 255) / 256 * gn,
-                          ncu, true, g, s);
-        MC_CHECK_LAUNCH("maeclip_gemm(v4, stream-K)");
         return 0;
       }
     }
@@ -1204,9 +1229,8 @@ int64_t gemm_v4_workspace(const maeclip_gemm_args& a) {
   maeclip_gemm_args b = a;
   b.workspace = (float*)(uintptr_t)256;   // any non-null: "a workspace is offered"
   const int ncu = gemm4_ncu();
-  return choose_tiles(b, f8 ? 128 : 64, ncu).sk.skw > 0 ? sk_workspace_bytes(ncu) : 0;
+  return choose_tiles(b, f8 ? 128 : 64, ncu).sk.on() ? sk_workspace_bytes(ncu) : 0;
 }
-int64_t gemm_sk_counter_bytes() { return SK_CNT_BYTES; }
 
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
   if (a.a_layout == LAY_KC && a.b_layout == LAY_KC) return out4<LAY_KC, LAY_KC>(a, s);
@@ -1217,10 +1241,6 @@ int gemm_v4(const maeclip_gemm_args& a, hipStream_t s) {
 }  // namespace maeclip
 
 // ------------------------------------------------------------ fp8 operands
-namespace maeclip {
-bool gemm_lib_fp8_ok(const maeclip_gemm_args& a);
-int gemm_lib(const maeclip_gemm_args& a, hipStream_t s, const float* scale_a, const float* scale_b);
-}  // namespace maeclip
 
 namespace {
 
@@ -1235,17 +1255,12 @@ int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipS
   if (a.batch == 1) {
     const TileChoice tc = choose_tiles(a, 128, ncu);
     g.sk = tc.sk;
-    const bool sk = tc.sk.skw > 0;
+    const bool sk = tc.sk.on();
     const int64_t tiles = (a.M + tc.bm - 1) / tc.bm * gn;
     if (tc.bm == 192) {
       if (sk) launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 192, true>, TileM<192>::LDS_ALL, tiles, ncu, true, g, s);
       else launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
       MC_CHECK_LAUNCH("maeclip_gemm_fp8(192-row tiles)");
-      return 0;
-    }
-    if (sk) {
-      launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 256, true>, TileM<256>::LDS_ALL, tiles, ncu, true, g, s);
-      MC_CHECK_LAUNCH("maeclip_gemm_fp8(stream-K)");
       return 0;
     }
   }
@@ -1301,14 +1316,6 @@ extern "C" int32_t maeclip_gemm_fp8(const maeclip_gemm_args* a, const float* sca
   const int64_t lim = 0x7fffffffLL;
   MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "maeclip_gemm_fp8: operand exceeds 2^31 bytes");
   hipStream_t s = (hipStream_t)stream;
-  // calibration only (MAECLIP_GEMM_LIB=1): the vendor library with
-  // outer-vector scales for the plain / residual forms (gemm_lib.hip)
-  if (maeclip::gemm_lib_fp8_ok(*a)) {
-    maeclip_gemm_args b = *a;
-    if (b.workspace) b.workspace = (float*)((char*)b.workspace + SK_CNT_BYTES);
-    const int rc = maeclip::gemm_lib(b, s, scale_a, scale_b);
-    if (rc != 1) return rc;
-  }
   const bool e5 = a->dtype == MAECLIP_FP8_E5M2;
   if (a->out_dtype == MAECLIP_BF16)
     return e5 ? epi_f8<bf16_t, 2>(*a, scale_a, scale_b, s) : epi_f8<bf16_t, 1>(*a, scale_a, scale_b, s);

@@ -118,8 +118,6 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
             nbytes += M * N * 4 * batch
         key = (f"M{M} N{N} K{K} {'KR'[a_layout]}{'KR'[b_layout]} epi{epilogue} "
                f"{'bf16' if A.dtype == torch.bfloat16 else 'f32'}>{'bf16' if Cout.dtype == torch.bfloat16 else 'f32'}")
-        if int(L.lib().maeclip_gemm_impl(C.byref(a))) == 1:
-            key += " [hipBLASLt]"   # the vendor library runs this launch (gemm_lib.hip)
         LAUNCH_HOOK(key, 2.0 * M * N * K * batch, nbytes, lambda: _call("maeclip_gemm", C.byref(a), _stream()))
 
 
@@ -225,7 +223,7 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
                    resid=_ptr(resid), ldr=(resid.stride(0) if resid is not None else 0),
                    colsum_partial=_ptr(colsum), splitk=1, workspace=None)
     nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
-    if nb > 0:   # the vendor library's workspace (gemm_lib.hip)
+    if nb > 0:   # the split plan's counters + partial tiles (per stream)
         a.workspace = _stream_scratch(A.q.device, nb).data_ptr()
     launch = lambda: _call("maeclip_gemm_fp8", C.byref(a), A.s.data_ptr(), B.s.data_ptr(), _stream())
     if LAUNCH_HOOK is None:
@@ -239,8 +237,6 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
     if resid is not None:
         nbytes += M * N * 4
     key = f"M{M} N{N} K{K} KK epi{epilogue} fp8{'e5' if A.fmt == FP8_E5M2 else 'e4'}>{'bf16' if ec == 2 else 'f32'}"
-    if int(L.lib().maeclip_gemm_impl(C.byref(a))) == 1:
-        key += " [hipBLASLt]"
     LAUNCH_HOOK(key, 2.0 * M * N * K, nbytes, launch)
     return Cout
 

@@ -10,15 +10,6 @@ from mae_clip_amd import kernels as K
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _own_gemm_kernels(monkeypatch, request):
-    """The GEMM tests here check this library's kernels: plain bf16 launches
-    would otherwise go to the vendor library (gemm_lib.hip), which
-    test_gemm_vendor_plain covers."""
-    if request.node.name.startswith("test_gemm") and "vendor" not in request.node.name:
-        monkeypatch.setenv("MAECLIP_GEMM_LIB", "0")
-
-
 def _rand(shape, dtype, dev, scale=1.0, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     return (torch.randn(shape, generator=g) * scale).to(dtype).to(dev)
@@ -77,21 +68,23 @@ def _sk_counters_zero():
 @pytest.mark.parametrize("b_lay", [0, 1])
 @pytest.mark.parametrize("mnk", [(6400, 768, 3072), (6400, 2304, 768), (25216, 512, 2048), (50432, 512, 1536),
                                  (1000, 520, 192), (300, 264, 640), (12800, 768, 768)])
-@pytest.mark.parametrize("mode", ["sk", "sk192", "auto"])
+@pytest.mark.parametrize("mode", ["auto", "split2_192", "split2_192_lead0", "split2_192_lead9"])
 def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
-    """Stream-K plain launches (the cut tiles summed in the same launch by the
-    block that arrives last, gemm4.hip sk_fixup): forced on every shape whose
-    tiles leave a partial last round ("sk"; "sk192" on 192-row tiles), or the
-    cost model's own choice ("auto"). Shapes: the micro-batch's encoder dgrads
-    (75 tiles for 256 CUs), the decoder's N = 512 dgrads (198 tiles; 394 =
-    one whole round + 138 stream-K tiles), tiny ragged launches where most
-    blocks get no K-tile and a tile is cut into up to 3 pieces of one K-tile.
+    """Split plain launches (every tile's K range cut into S slices, the
+    slices summed in the same launch by the block that arrives last, gemm4.hip
+    sk_fixup): forced on 192-row tiles ("split2_192", slice 0's lead per
+    other slice 4 K-tiles by default, 0 = equal slices, 9) or the cost model's
+    own choice ("auto"). Shapes: the micro-batch's encoder dgrads
+    (75 tiles for 256 CUs), the decoder's N = 512 dgrads (198 tiles: 396
+    units of S = 2 = two rounds of the grid), small ragged launches (slices of
+    one or two K-tiles, partial edge tiles).
     vs fp64; bitwise equal on repeat (the summation order is fixed whichever
     block arrives last); counters left zero."""
-    if mode != "auto":
-        monkeypatch.setenv("MAECLIP_GEMM_SK", "1")
-    if mode == "sk192":
+    if mode.startswith("split"):
+        monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
         monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    if "_lead" in mode:
+        monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
     M, N, Kd = mnk
     A = _rand((M, Kd), torch.bfloat16, dev, seed=11)
     B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, scale=0.5, seed=12)
@@ -109,15 +102,16 @@ def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
     _sk_counters_zero()
 
 
-@pytest.mark.parametrize("mode", ["sk", "sk192"])
+@pytest.mark.parametrize("mode", ["split2_192", "split2_192_lead0"])
 def test_gemm_stream_k_epilogues(dev, mode, monkeypatch):
-    """Every fused epilogue behind the stream-K fix-up (the last block runs it
+    """Every fused epilogue behind the split fix-up (the last block runs it
     on the summed tile): bias + GELU / GELU' (aux_out), fp32 residual, column
     sums, dGELU, mul-aux + residual; M = 3000 x N = 768 (36 / 48 tiles, every
     tile cut) at K = 1024."""
-    monkeypatch.setenv("MAECLIP_GEMM_SK", "1")
-    if mode == "sk192":
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
+    monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    if "_lead" in mode:
+        monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
     M, N, Kd = 3000, 768, 1024
     x = _rand((M, Kd), torch.bfloat16, dev, seed=13)
     w = _rand((N, Kd), torch.bfloat16, dev, scale=0.03, seed=14)
@@ -870,61 +864,3 @@ def test_combined_loss_backward_matches_torch(dev):
     assert torch.allclose(T.grad, 3.0 * dT, rtol=1e-6, atol=1e-9)
 
 
-@pytest.mark.parametrize("mnk", [(6400, 2304, 768), (6400, 768, 3072), (25216, 512, 2048), (1000, 520, 192), (256, 256, 64)])
-@pytest.mark.parametrize("b_lay", [0, 1])
-def test_gemm_vendor_plain(dev, mnk, b_lay, monkeypatch):
-    """Plain bf16 GEMMs (no epilogue) through the vendor library
-    (gemm_lib.hip, the default) against this library's v4 kernel
-    (MAECLIP_GEMM_LIB=0) and fp64, bf16 and f32 outputs, KC and RC B, alpha 0.5;
-    the vendor path is deterministic run to run."""
-    M, N, Kd = mnk
-    A = _rand((M, Kd), torch.bfloat16, dev, seed=11)
-    B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, seed=12)
-    ref = 0.5 * _ref_mm(A, B.t() if b_lay == 0 else B)
-    scale = ref.abs().max().item()
-    for out in (torch.bfloat16, torch.float32):
-        res = {}
-        for mode in ("1", "1", "0"):
-            monkeypatch.setenv("MAECLIP_GEMM_LIB", mode)
-            C = torch.full((M, N), float("nan"), device=dev, dtype=out)
-            K.gemm(A, B, C, M, N, Kd, A.stride(0), B.stride(0), N, 0, b_lay, alpha=0.5)
-            torch.cuda.synchronize()
-            if mode in res:
-                assert torch.equal(res[mode], C), (out, "vendor path not deterministic")
-            res[mode] = C
-        tol = (1e-2 if out == torch.bfloat16 else 2e-5 * math.sqrt(Kd)) * scale
-        for mode, C in res.items():
-            assert torch.isfinite(C).all(), (mode, out)
-            assert (C.double() - ref).abs().max().item() < tol, (mode, out)
-
-
-@pytest.mark.parametrize("mnk", [(6400, 768, 3072), (25216, 512, 2048), (1000, 264, 768)])
-def test_gemm_vendor_bias_resid(dev, mnk, monkeypatch):
-    """The vendor path's epilogues (gemm_lib.hip): bias on a bf16 C and the
-    residual form C = x W^T + b + R (fp32 R and C), against the own kernel
-    (MAECLIP_GEMM_LIB=0) and fp64; the K = 512 rule sends a 512-deep launch to
-    the own kernel (checked by equality with MAECLIP_GEMM_LIB=0)."""
-    M, N, Kd = mnk
-    x = _rand((M, Kd), torch.bfloat16, dev, seed=21)
-    w = _rand((N, Kd), torch.bfloat16, dev, scale=0.05, seed=22)
-    bias = _rand((N,), torch.float32, dev, seed=23)
-    resid = _rand((M, N), torch.float32, dev, seed=24)
-    ref = _ref_mm(x, w.t()) + bias.double()
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MAECLIP_GEMM_LIB", mode)
-        y = K.linear_fwd(x, w, bias)
-        r = K.linear_fwd(x, w, bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=resid)
-        torch.cuda.synchronize()
-        out[mode] = (y, r)
-    scale = ref.abs().max().item()
-    for mode, (y, r) in out.items():
-        assert (y.double() - ref).abs().max().item() < 1e-2 * scale, mode
-        assert (r.double() - (ref + resid.double())).abs().max().item() < 2e-5 * math.sqrt(Kd) * scale, mode
-    x5 = _rand((M, 512), torch.bfloat16, dev, seed=25)
-    w5 = _rand((N, 512), torch.bfloat16, dev, scale=0.05, seed=26)
-    y5 = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MAECLIP_GEMM_LIB", mode)
-        y5[mode] = K.linear_fwd(x5, w5, bias)
-    assert torch.equal(y5["1"], y5["0"])

@@ -638,7 +638,6 @@ def test_stack_microbatches_match_whole_batch(dev, monkeypatch):
     micro-batch and whole-batch GEMMs would agree only to rounding
     (test_gemm_stream_k checks stream-K itself; the captured micro-batched
     step with the default settings: test_captured_step_matches_eager_microbatched)."""
-    monkeypatch.setenv("MAECLIP_GEMM_LIB", "0")
     monkeypatch.setenv("MAECLIP_GEMM_SK", "0")
     from tests.helpers import product_config
     from mae_clip_amd.CLIP import CLIPModel

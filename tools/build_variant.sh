@@ -18,5 +18,5 @@ for f in "$V"/mae_clip_amd/csrc/*.hip; do
   /opt/rocm/bin/hipcc $FLAGS -c "$f" -o "$V/obj/$b.o" & pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$V"/obj/*.o -o "$ROOT/mae_clip_amd/libmaeclip_$NAME.so" -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC "$V"/obj/*.o -o "$ROOT/mae_clip_amd/libmaeclip_$NAME.so"
 echo "built mae_clip_amd/libmaeclip_$NAME.so"

@@ -12,6 +12,5 @@ mkdir -p "$O"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wall -Wno-unused-function "$@" \
   -c "$ROOT/mae_clip_amd/csrc/gemm4.hip" -o "$O/gemm4.o"
 objs=$(ls "$ROOT"/build/obj/*.o | grep -v '/gemm4.o$')
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs "$O/gemm4.o" -o "$ROOT/mae_clip_amd/libmaeclip_$NAME.so" \
-  -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs "$O/gemm4.o" -o "$ROOT/mae_clip_amd/libmaeclip_$NAME.so"
 echo "built mae_clip_amd/libmaeclip_$NAME.so"

@@ -1,10 +1,12 @@
-"""Per-shape timing of the GEMM launches the vendor path used to take (round 4's
-plain_gemm_vendor_probe rows + the fp32 residual forms), micro-batch (B=128)
-and whole-batch (B=256) row counts of the C2 step: this library's kernel with
-its default tile / stream-K choice ("own"), the same with stream-K off
-("own_dp"), and hipBLASLt through the calibration switch (MAECLIP_GEMM_LIB=3:
-every K). One process, interleaved rounds, median per-launch time (µs).
-One JSON line per shape. Calibration only: the product never runs hipBLASLt."""
+"""Per-shape timing of the plain / residual-form GEMM launches the round-4
+vendor path used to take (round 4's plain_gemm_vendor_probe rows + the fp32
+residual forms), micro-batch (B=128) and whole-batch (B=256) row counts of the
+C2 step: this library's kernel with its default tile / split choice ("own"),
+the same with the split off ("own_dp"), and torch's bf16 matmul ("vendor":
+hipBLASLt through torch, calibration only -- the product never calls it; for
+the residual forms it is the plain bf16 product, without the fp32 residual
+read / fp32 store of the own launch). One process, interleaved rounds, median
+per-launch time (us). One JSON line per shape."""
 import json
 import os
 import statistics
@@ -15,9 +17,7 @@ import torch
 from mae_clip_amd import kernels as K
 
 dev = torch.device("cuda")
-MODES = {"own": {"MAECLIP_GEMM_LIB": "0", "MAECLIP_GEMM_SK": ""},
-         "own_dp": {"MAECLIP_GEMM_LIB": "0", "MAECLIP_GEMM_SK": "0"},
-         "vendor": {"MAECLIP_GEMM_LIB": "3", "MAECLIP_GEMM_SK": ""}}
+MODES = {"own": {"MAECLIP_GEMM_SK": ""}, "own_dp": {"MAECLIP_GEMM_SK": "0"}, "vendor": None}
 
 
 def shapes(B):
@@ -44,7 +44,7 @@ def time_one(fn, reps=20):
 
 
 def setenv(mode):
-    for k, v in MODES[mode].items():
+    for k, v in (MODES[mode] or {}).items():
         if v:
             os.environ[k] = v
         else:
@@ -63,23 +63,28 @@ for B in (128, 256):
         bias = torch.randn(N, generator=g).to(dev) if (res or lb == 0) else None
         R = torch.randn(M, N, generator=g).to(dev) if res else None
         C = torch.empty(M, N, device=dev, dtype=torch.float32 if res else torch.bfloat16)
+        Cv = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        Bt = Bm.t() if lb == 0 else Bm
         epi = K.EPI_RESID if res else K.EPI_NONE
-        fn = lambda: K.gemm(A, Bm, C, M, N, Kd, A.stride(0), Bm.stride(0), N, 0, lb, epilogue=epi, bias=bias,
-                            resid=R, ldr=N if res else 0)
+        own = lambda: K.gemm(A, Bm, C, M, N, Kd, A.stride(0), Bm.stride(0), N, 0, lb, epilogue=epi, bias=bias,
+                             resid=R, ldr=N if res else 0)
+        vendor = lambda: torch.matmul(A, Bt, out=Cv)
         t = {m: [] for m in MODES}
         outs = {}
         for m in MODES:
             setenv(m)
+            fn = vendor if MODES[m] is None else own
             fn()
             fn()
             torch.cuda.synchronize()
-            outs[m] = C.float().clone()
+            outs[m] = (Cv if MODES[m] is None else C).float().clone()
         for r in range(5):
             for m in MODES:
                 setenv(m)
-                t[m].append(time_one(fn))
+                t[m].append(time_one(vendor if MODES[m] is None else own))
         med = {m: statistics.median(v) for m, v in t.items()}
-        dev_own = ((outs["own"] - outs["vendor"]).abs().max() / outs["vendor"].abs().max()).item()
+        ref = outs["vendor"] + (R + bias if res else 0)
+        dev_own = ((outs["own"] - ref).abs().max() / ref.abs().max()).item()
         print(json.dumps(dict(B=B, name=name, M=M, N=N, K=Kd, own_us=round(med["own"], 1),
                               own_dp_us=round(med["own_dp"], 1), vendor_us=round(med["vendor"], 1),
                               own_vs_vendor=round(med["vendor"] / med["own"], 3), max_rel_diff=dev_own)), flush=True)

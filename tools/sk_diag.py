@@ -25,6 +25,11 @@ SHAPES = [  # name, M, N, K, b_layout, epilogue
     ("enc qkv dgrad", 6400, 768, 2304, 1, K.EPI_NONE),
     ("enc proj fwd+res", 6400, 768, 768, 0, K.EPI_RESID),
     ("dec fc1 dgrad", 25216, 512, 2048, 1, K.EPI_NONE),
+    ("dec qkv dgrad", 25216, 512, 1536, 1, K.EPI_NONE),
+    ("text lin2 fwd+res", 3200, 768, 3072, 0, K.EPI_RESID),
+    ("enc qkv fwd", 6400, 2304, 768, 0, K.EPI_NONE),
+    ("enc fc1 dgrad B256", 12800, 768, 3072, 1, K.EPI_NONE),
+    ("enc fc2 fwd+res B256", 12800, 768, 3072, 0, K.EPI_RESID),
 ]
 only = os.environ.get("ONLY")
 
@@ -52,14 +57,20 @@ def time_one(fn, reps=10):
     return s.elapsed_time(e) / reps * 1e3
 
 
-MODES = {"dp": "0", "sk": "1", "auto": ""}
+MODES = {"dp": {"MAECLIP_GEMM_SK": "0"}, "auto": {}, "dp256": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "256"},
+         "dp192": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "192"}}
+for d in (0, 2, 4, 6, 8):
+    MODES[f"split2_192_d{d}"] = {"MAECLIP_GEMM_SPLIT": "2", "MAECLIP_GEMM_BM": "192", "MAECLIP_GEMM_SPLIT_D": str(d)}
+if os.environ.get("SKMODES"):
+    MODES = {k: v for k, v in MODES.items() if k in os.environ["SKMODES"].split(",")}
 
 
 def setmode(v):
-    if v:
-        os.environ["MAECLIP_GEMM_SK"] = v
-    else:
-        os.environ.pop("MAECLIP_GEMM_SK", None)
+    for k in ("MAECLIP_GEMM_SK", "MAECLIP_GEMM_BM", "MAECLIP_GEMM_SPLIT", "MAECLIP_GEMM_SPLIT_D"):
+        os.environ.pop(k, None)
+    if isinstance(v, str):
+        v = {"MAECLIP_GEMM_SK": v}
+    os.environ.update(v)
 
 
 for name, M, N, Kd, lb, epi in SHAPES:
@@ -78,7 +89,8 @@ for name, M, N, Kd, lb, epi in SHAPES:
             setmode(v)
             t[m].append(time_one(fn))
     med = {m: round(statistics.median(x), 1) for m, x in t.items()}
-    diff = max(((outs[m] - outs["dp"]).abs().max() / outs["dp"].abs().max()).item() for m in MODES)
+    ref = outs[next(iter(MODES))]
+    diff = max(((outs[m] - ref).abs().max() / ref.abs().max()).item() for m in MODES)
     rec = dict(lib=label, name=name, M=M, N=N, K=Kd, us=med, max_rel_diff_vs_dp=diff)
     if os.environ.get("STAMPS") and hasattr(lib, "maeclip_debug_gemm4_stamps"):
         f = lib.maeclip_debug_gemm4_stamps
