@@ -34,6 +34,16 @@
 namespace {
 
 constexpr int MAXW = 8;          // max waves per workgroup (sized per launch to the tile count)
+// forward waves per SIMD the register allocator must keep: the bf16 HD 32
+// body with the MFMA row sum fits 80 VGPRs (6 waves per SIMD, 3 workgroups of
+// 7 waves per CU at n = 197); the others are left to the compiler
+template <typename T, int HD, bool DROP> constexpr int fwd_wpe() {
+#ifdef FWD_WPE
+  return FWD_WPE;
+#else
+  return (sizeof(T) == 2 && HD == 32 && !DROP) ? 6 : 1;
+#endif
+}
 
 bool getenv_flag(const char* name) {
   const char* v = getenv(name);
@@ -299,10 +309,17 @@ struct FwdDrop {
 // MASKED: add the key bias (padding keys, DistilBERT's key mask) -- the scale
 // c > 0 then rides in the bias fma, otherwise in the exponent's fma and the
 // running max is taken on the raw scores.
+// bf16 without dropout: the row sum of P comes out of the MFMA as a
+// 17th..32nd "V column" of ones (lsum accumulator `ol`, every element the
+// lane's query's sum of the bf16 P the PV product uses) instead of 16 VALU
+// adds per chunk -- the kernel is VALU-bound at HD 32, the MFMA pipe is not;
+// lsum is then the exact weight sum of O = sum P V (both over bf16(P)).
+// With dropout the normalisation needs the sum BEFORE the mask: VALU adds.
 template <typename T, int HD, int NH, bool MASKED, bool DROP>
 __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, const float* kmask, int kc,
                                           const RowFrag<T, HD> (&qf)[HD / 32], float c, float& m, float& lsum,
-                                          v4f (&o)[HD / 16], int lane, const FwdDrop& dr, int q) {
+                                          v4f (&o)[HD / 16], v4f& ol, int lane, const FwdDrop& dr, int q) {
+  constexpr bool MSUM = std::is_same<T, bf16_t>::value && !DROP;
   const int g = lane >> 4;
   v4f s[2 * NH];
 #pragma unroll
@@ -343,10 +360,14 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], cc, nm));
-      lp += p;
+      if (!MSUM) lp += p;
       s[t][i] = p;
     }
-  lsum = fmaf(lsum, alpha, lp);
+  if (MSUM) {
+    ol[0] *= alpha;   // only element 0 is read back
+  } else {
+    lsum = fmaf(lsum, alpha, lp);
+  }
 #pragma unroll
   for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
   m = mnew;
@@ -360,14 +381,20 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
       }
   }
 #pragma unroll
-  for (int s2 = 0; s2 < NH; ++s2)
+  for (int s2 = 0; s2 < NH; ++s2) {
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt)
       o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
+    if constexpr (MSUM) {
+      const v8s ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};   // bf16 1.0
+      ol = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pack_p(s[2 * s2], s[2 * s2 + 1]), ol, 0, 0, 0);
+    }
+  }
 }
 
 template <typename T, int HD, bool DROP>
-__global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_args a) {
+__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(fwd_wpe<T, HD, DROP>())))
+attn_fwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
@@ -415,18 +442,21 @@ __global__ void __launch_bounds__(MAXW * 64) attn_fwd_kernel(const maeclip_attn_
     for (int ks = 0; ks < HD / 32; ++ks) qf[ks].glob(qkv + (int64_t)q * a.ld_qkv + h * HD, ks, lane, qok);
 
     float m = NEG_BIG, lsum = 0.f;
-    v4f o[HD / 16];
+    v4f o[HD / 16], ol = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) o[dt] = v4f{0.f, 0.f, 0.f, 0.f};
 
     int kc = 0;
-    for (; kc < 64 * nfull; kc += 64) fwd_chunk<T, HD, 2, false, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
+    for (; kc < 64 * nfull; kc += 64)
+      fwd_chunk<T, HD, 2, false, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
     for (; kc < npad; kc += 64) {
       // 32-key halves of this chunk that hold real keys (wave-uniform)
-      if (n - kc > 32) fwd_chunk<T, HD, 2, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
-      else fwd_chunk<T, HD, 1, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, lane, dr, q);
+      if (n - kc > 32) fwd_chunk<T, HD, 2, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
+      else fwd_chunk<T, HD, 1, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
     }
-    lsum = sum4rows(lsum);
+    // the MFMA row sum (bf16, no dropout) is whole in every lane of the query
+    if (std::is_same<T, bf16_t>::value && !DROP) lsum = ol[0];
+    else lsum = sum4rows(lsum);
     const float inv = 1.f / lsum;
     if (qok) {
       T* orow = (T*)a.o + ((int64_t)b * n + q) * a.ld_o + h * HD;

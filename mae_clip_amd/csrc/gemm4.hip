@@ -1051,8 +1051,8 @@ int gemm4_ncu() {
 // encoder fc2 fwd, one round each); a tile's epilogue ~EPI_C; a split costs
 // slice 0's K-tiles (its lead hides the others' publish) + F1 per other slice
 // the last block reads back. MAECLIP_GEMM_BM=256 / 192 forces a tile height;
-// MAECLIP_GEMM_SK=0 disables the split; MAECLIP_GEMM_SPLIT=S forces a split
-// of S wherever it fits (A/B, tests).
+// MAECLIP_GEMM_SK=1 enables the cost model's split (default off, see below);
+// MAECLIP_GEMM_SPLIT=S forces a split of S wherever it fits (A/B, tests).
 struct TileChoice {
   int bm;
   SkPlan sk;
@@ -1063,7 +1063,9 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
   const char* eb = getenv("MAECLIP_GEMM_BM");
   const int force_bm = (eb && *eb) ? atoi(eb) : 0;
   const char* es = getenv("MAECLIP_GEMM_SK");
-  const int sk_mode = (es && *es) ? atoi(es) : 1;   // 0 off, 1 cost model
+  // default off: in the micro-batched step every split cost whole-step
+  // throughput although it wins alone (profiles/r05/gemm_split_minK_step_ab_r5i.txt)
+  const int sk_mode = (es && *es) ? atoi(es) : 0;   // 0 off, 1 cost model
   const char* esp = getenv("MAECLIP_GEMM_SPLIT");
   const int force_split = (esp && *esp) ? atoi(esp) : 0;
   // the cost model's split only at K >= MAECLIP_GEMM_SPLIT_MINK (step A/B)

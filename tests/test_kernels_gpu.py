@@ -83,6 +83,8 @@ def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
     if mode.startswith("split"):
         monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
         monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    else:
+        monkeypatch.setenv("MAECLIP_GEMM_SK", "1")   # the cost model (off by default)
     if "_lead" in mode:
         monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
     M, N, Kd = mnk
