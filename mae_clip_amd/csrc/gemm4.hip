@@ -130,6 +130,18 @@ __device__ __forceinline__ v8s frag(const char* lds, int rs, int ks, int lane) {
   }
 }
 
+// p1 / p2 reads (Bn1, Am1) are restaged two phases after they are read, so
+// they need not be retired before the barrier that ends their segment
+// (cdna_hip_programming.md §5, 256^2 template, WAR rule); GEMM4_LATE_LGKM
+// leaves their wait to the compiler's, right before the first MFMA that uses
+// them, so the read latency overlaps the barrier. p0's reads (Am0, restaged
+// one phase later) keep the early wait.
+#ifdef GEMM4_LATE_LGKM
+#define LGKM_EARLY() do {} while (0)
+#else
+#define LGKM_EARLY() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#endif
+
 #define SEG_BARRIER()                        \
   do {                                       \
     asm volatile("" ::: "memory");           \
@@ -151,6 +163,31 @@ __device__ __forceinline__ v8i cat_frag(v8s a, v8s b) {
   const v4i x = __builtin_bit_cast(v4i, a), y = __builtin_bit_cast(v4i, b);
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// Keep a quadrant's MFMAs inside their segment: an empty asm that reads and
+// writes the quadrant's accumulators cannot be reordered with the asm barrier
+// that follows, so every MFMA of the cluster is emitted before it. Without
+// it hipcc (ROCm 7.2) moved 10 of the 16 MFMAs of p0 and of p1 past the
+// segment's closing s_barrier into the next read segment (tools/isa_gemm4.sh
+// + the per-segment MFMA count), undoing the ping-pong (GEMM4_NO_PIN restores
+// that schedule for A/B). Measured (profiles/r05/gemm_pin_ab_r5n.txt): every
+// plain shape 1.02-1.17x (4096^3 1109 -> 1292 TF/s), the C2 step 9963 ->
+// 10221 img/s. In the grouped weight-gradient body GEMM4_PIN_GRP is a bit
+// mask of the phases p0..p3 pinned: all four make its RC x RC fragment
+// addresses spill inside the K loop (2790 instead of 2450 us per launch);
+// p0 + p1 (the two clusters the compiler split) alone keep every cluster
+// whole with the unpinned body's spills (one scratch reload per K-tile):
+// step 10150 -> 10254 img/s on one box (profiles/r05/step_pinmask_ab_r5p.txt).
+#ifndef GEMM4_PIN_GRP
+#define GEMM4_PIN_GRP 3
+#endif
+template <int MI>
+__device__ __forceinline__ void pin_quad(v4f (&acc)[2 * MI][4], int i0, int j0) {
+#ifndef GEMM4_NO_PIN
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(acc[i0 + i][j0]), "+v"(acc[i0 + i][j0 + 1]));
+#endif
+}
+
 template <int F8, int MI>
 __device__ __forceinline__ void quad_mma(v4f (&acc)[2 * MI][4], int i0, int j0, const v8s (&fbq)[2][2],
                                          const v8s (&fa)[MI][2]) {
@@ -878,6 +915,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
       quad_mma<F8, MI>(acc, 0, 0, fb[0], fa);
+      if constexpr (!GRP || (GEMM4_PIN_GRP >> 0) & 1) pin_quad<MI>(acc, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p1: quadrant (0,1)
@@ -886,10 +924,11 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = frag<LB>(hB1, 32 * wn + 16 * j, ks, lane);
       if (more2) issue(u, voA, voB, t + 2, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      LGKM_EARLY();
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
       quad_mma<F8, MI>(acc, 0, 2, fb[1], fa);
+      if constexpr (!GRP || (GEMM4_PIN_GRP >> 1) & 1) pin_quad<MI>(acc, 0, 2);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p2: quadrant (1,1)
@@ -898,10 +937,11 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, (BM / 4) * wm + 16 * i, ks, lane);
       if (more2) issue(u, voA, voB, t + 2, 2);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      LGKM_EARLY();
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
       quad_mma<F8, MI>(acc, MI, 2, fb[1], fa);
+      if constexpr (!GRP || (GEMM4_PIN_GRP >> 2) & 1) pin_quad<MI>(acc, MI, 2);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
       // ---- p3: quadrant (1,0), operands already in VGPRs. Every LDS read of
@@ -923,6 +963,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
       quad_mma<F8, MI>(acc, MI, 0, fb[0], fa);
+      if constexpr (!GRP || (GEMM4_PIN_GRP >> 3) & 1) pin_quad<MI>(acc, MI, 0);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 || more1) SEG_BARRIER();   // group 1 skips its very last one (it took one extra up front)
     }

@@ -21,7 +21,14 @@ items = []
 for _ in range(8):
     for n, k in ((D, F), (F, D), (D, D), (3 * D, D)):   # fc2, fc1, proj, qkv
         items.append((mk(M, n), mk(M, k), torch.empty(n, k, device=dev)))
+ts = []
 for _ in range(reps):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
     K.wgrad_grouped(items)
+    e.record()
+    ts.append((s, e))
 torch.cuda.synchronize()
-print("ok", len(items), "problems,", reps, "launches")
+us = sorted(s.elapsed_time(e) * 1e3 for s, e in ts)[len(ts) // 2]
+flops = sum(2.0 * M * it[0].shape[1] * it[1].shape[1] for it in items)
+print("ok", len(items), "problems,", reps, "launches, median", round(us, 1), "us,", round(flops / us / 1e6, 1), "TF/s")
