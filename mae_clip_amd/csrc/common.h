@@ -141,6 +141,28 @@ __device__ __forceinline__ void gelu_pair(float x, float& y, float& dy) {
   y = x * cdf;
   dy = fmaf(x * e, 0.39894228040143268f, cdf);
 }
+// The same pair for two values at once: every add / mul / fma of the erfc
+// polynomial on a float2, which gfx950 issues as one v_pk_* instruction for
+// both (no MFMA beside it in a GEMM epilogue, where the GELU math is the
+// VALU-bound part); the two rcp / exp stay per value. Same formula, so the
+// result is the scalar pair's to within the packed ops' rounding (identical
+// operations: bitwise equal on gfx950).
+__device__ __forceinline__ void gelu_pair2(mc_f32x2 x, mc_f32x2& y, mc_f32x2& dy) {
+  const mc_f32x2 ax = {fabsf(x[0]), fabsf(x[1])};
+  const mc_f32x2 z = ax * 0.70710678118654752f;
+  const mc_f32x2 den = __builtin_elementwise_fma(z, (mc_f32x2){0.3275911f, 0.3275911f}, (mc_f32x2){1.0f, 1.0f});
+  const mc_f32x2 t = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+  const mc_f32x2 h = (x * x) * -0.5f;
+  const mc_f32x2 e = {__expf(h[0]), __expf(h[1])};
+  mc_f32x2 p = __builtin_elementwise_fma(t, (mc_f32x2){1.061405429f, 1.061405429f}, (mc_f32x2){-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(t, p, (mc_f32x2){1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(t, p, (mc_f32x2){-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(t, p, (mc_f32x2){0.254829592f, 0.254829592f});
+  const mc_f32x2 ht = ((p * t) * e) * 0.5f;              // 0.5 erfc(|x|/sqrt2)
+  const mc_f32x2 cdf = {x[0] < 0.f ? ht[0] : 1.0f - ht[0], x[1] < 0.f ? ht[1] : 1.0f - ht[1]};
+  y = x * cdf;
+  dy = __builtin_elementwise_fma(x * e, (mc_f32x2){0.39894228040143268f, 0.39894228040143268f}, cdf);
+}
 // gelu and gelu' of the 4 lanes of v: v <- gelu(v), returns gelu'(v)
 __device__ __forceinline__ v4f gelu4_inplace(v4f& v) {
   v4f d;

@@ -409,11 +409,14 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
         float d[VPL];   // GELU: aux_out <- pre-activation; GELU_D: aux_out <- gelu'(pre)
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-          float y, dy;
-          gelu_pair(x[v], y, dy);
-          d[v] = EPI == EPI_GELU_D ? dy : x[v];
-          x[v] = y;
+        for (int v = 0; v < VPL; v += 2) {   // value pairs: packed f32 math (gelu_pair2)
+          mc_f32x2 y, dy;
+          const mc_f32x2 xv = {x[v], x[v + 1]};
+          gelu_pair2(xv, y, dy);
+          d[v] = EPI == EPI_GELU_D ? dy[0] : x[v];
+          d[v + 1] = EPI == EPI_GELU_D ? dy[1] : x[v + 1];
+          x[v] = y[0];
+          x[v + 1] = y[1];
         }
         if (args.aux_out && ok) {
           bf16_t* ap = (bf16_t*)args.aux_out + off + (int64_t)m * args.ldaux + n;
