@@ -83,7 +83,7 @@ for B in (128, 256):
                 setenv(m)
                 t[m].append(time_one(vendor if MODES[m] is None else own))
         med = {m: statistics.median(v) for m, v in t.items()}
-        ref = outs["vendor"] + (R + bias if res else 0)
+        ref = outs["vendor"] + (R if res else 0) + (bias if bias is not None else 0)
         dev_own = ((outs["own"] - ref).abs().max() / ref.abs().max()).item()
         print(json.dumps(dict(B=B, name=name, M=M, N=N, K=Kd, own_us=round(med["own"], 1),
                               own_dp_us=round(med["own_dp"], 1), vendor_us=round(med["vendor"], 1),
