@@ -62,10 +62,13 @@ template <int BM> struct TileM {
 };
 
 // local index l (0..127) of a half -> offset inside the 256-wide block tile
+// (BM = 192: local row l of a 96-row half; BM = 128: of a 64-row half; the
+// wave row group wm owns rows [BM/2 wm, BM/2 (wm + 1)), half `sub` its
+// sub-rows BM/4 sub .. +BM/4)
 template <int BM = 256>
 __device__ __forceinline__ int amap(int l, int sub) {
   if constexpr (BM == 256) return (l & 63) + ((l >> 6) << 7) + (sub << 6);
-  else return (l < 48 ? l : l + 48) + sub * 48;   // local row l of a 96-row half
+  else return (l % (BM / 4)) + (l / (BM / 4)) * (BM / 2) + sub * (BM / 4);
 }
 __device__ __forceinline__ int bmap(int l, int sub) { return (l & 31) + ((l >> 5) << 6) + (sub << 5); }
 
@@ -654,7 +657,8 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
                                            const float* __restrict__ sa = nullptr,
                                            const float* __restrict__ sb = nullptr, const SkPlan* skp_ = nullptr) {
   static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
-  static_assert(BM == 256 || (BM == 192 && LA == LAY_KC && !SPLIT && !GRP), "BM 192: KC A, plain launches only");
+  static_assert(BM == 256 || ((BM == 192 || BM == 128) && LA == LAY_KC && !SPLIT && !GRP),
+                "BM 192 / 128: KC A, plain launches only");
   static_assert(!SK || (!SPLIT && !GRP), "stream-K: plain launches only");
   using TM = TileM<BM>;
   constexpr int MI = TM::MI;
@@ -808,10 +812,11 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       if constexpr (BM == 256) {
         issue_half(rs, vA[h][0], vA[h][1], k0 * (LA == LAY_KC ? ESZ : (int)(w.lda * ESZ)), dst, wave);
       } else {
-        // a 96-row A half is 12 wave-instructions: waves 0-3 issue two, 4-7 one
+        // a 96-row A half is 12 wave-instructions (waves 0-3 issue two, 4-7
+        // one), a 64-row half 8 (one per wave)
         const int soff = k0 * ESZ;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + wave * 1024), 16, vA[h][0], soff, 0, 0);
-        if (wave < 4)
+        if (BM == 192 && wave < 4)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + (8 + wave) * 1024), 16, vA[h][1], soff, 0, 0);
       }
     } else {
@@ -837,9 +842,10 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
 
   bool primed = false, first = true, prev_full = false;
   // everything but the three youngest halves (Am0, Bn0, Bn1 of one K-tile):
-  // 2 + 2 + 2 wave-instructions, or 1 + 2 + 2 for waves 4-7 at BM 192
+  // 2 + 2 + 2 wave-instructions, or 1 + 2 + 2 for waves 4-7 at BM 192 and
+  // every wave at BM 128
   auto wait_halves = [&]() {
-    if (BM == 256 || wave < 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (BM == 256 || (BM == 192 && wave < 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   };
 #ifdef GEMM4_STAMPS
@@ -874,6 +880,10 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
         if (sizeof(OutT) == 2 && two_out) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
         else if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else if (BM == 128) {   // 4 row fragments x 2 (bf16) or x 4 (fp32) stores
+        if (sizeof(OutT) == 2 && two_out) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       } else if (sizeof(OutT) == 2 && two_out) {
         asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       } else {   // 6 row fragments x 2 (bf16) or x 4 (fp32) stores
@@ -1116,8 +1126,13 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
   const char* emk = getenv("MAECLIP_GEMM_SPLIT_MINK");
   const int64_t split_min_k = (emk && *emk) ? atoll(emk) : 0;
   const bool plain = a.splitk <= 1 && a.batch == 1;
-  const bool allow192 = force_bm != 256 && plain && a.a_layout == LAY_KC && !a.colsum_partial;
-  const bool allow256 = force_bm != 192 || !allow192;
+  const bool allow192 = force_bm != 256 && force_bm != 128 && plain && a.a_layout == LAY_KC && !a.colsum_partial;
+  // 128-row tiles: bf16 only (KT 64); chosen by the cost model only when
+  // MAECLIP_GEMM_BM128=1 (A/B) or forced by MAECLIP_GEMM_BM=128
+  const char* e128 = getenv("MAECLIP_GEMM_BM128");
+  const bool allow128 = KT == 64 && plain && a.a_layout == LAY_KC && !a.colsum_partial &&
+                        (force_bm == 128 || (force_bm == 0 && e128 && *e128 == '1'));
+  const bool allow256 = (force_bm != 192 || !allow192) && (force_bm != 128 || !allow128);
   const bool allow_sk = plain && sk_mode != 0 && a.workspace != nullptr && ncu <= 256;
   const int64_t gn = (a.N + 255) / 256, NT = a.K / KT;
   constexpr double EPI_C = 2.5, F1 = 2.0;
@@ -1143,9 +1158,9 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
     p.slots = (float*)((char*)a.workspace + SK_CNT_BYTES);
     return p;
   };
-  for (int bm : {256, 192}) {
-    if ((bm == 256 && !allow256) || (bm == 192 && !allow192)) continue;
-    const double c = bm == 192 ? 0.89 : 1.0;
+  for (int bm : {256, 192, 128}) {
+    if ((bm == 256 && !allow256) || (bm == 192 && !allow192) || (bm == 128 && !allow128)) continue;
+    const double c = bm == 192 ? 0.89 : bm == 128 ? 0.72 : 1.0;
     const int64_t T = (a.M + bm - 1) / bm * gn, R = T % ncu;
     const double dp = (double)((T + ncu - 1) / ncu) * (NT * c + EPI_C);
     if (dp < best_cost - 1e-9 && force_split == 0) {
@@ -1195,6 +1210,12 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
         if (sk) launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192, true>, TileM<192>::LDS_ALL, tiles, ncu, true, g, s);
         else launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
         MC_CHECK_LAUNCH("maeclip_gemm(v4, 192-row tiles)");
+        return 0;
+      }
+      if (tc.bm == 128) {
+        const int64_t tiles = (a.M + 127) / 128 * gn;
+        launch_persistent(gemm4_kernel<LA, LB, OutT, EPI, false, 128>, TileM<128>::LDS_ALL, tiles, ncu, false, g, s);
+        MC_CHECK_LAUNCH("maeclip_gemm(v4, 128-row tiles)");
         return 0;
       }
     }

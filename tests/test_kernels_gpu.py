@@ -41,10 +41,11 @@ def test_gemm_layouts(dev, dtype, lay, mnk):
 @pytest.mark.parametrize("b_lay", [0, 1])
 @pytest.mark.parametrize("mnk", [(12800, 768, 768), (1000, 520, 192), (50000, 512, 256), (192, 256, 64), (193, 264, 128),
                                  (12800, 3072, 768), (6400, 768, 3072), (300, 264, 64)])
-def test_gemm_bm192(dev, b_lay, mnk, monkeypatch):
-    """192-row tiles of the v4 kernel (forced): ragged M / N, one tile, several persistent tiles per block
-    (M = 50000: 261 x 2 tiles on 256 CUs), one K-tile, KC x KC and KC x RC."""
-    monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+@pytest.mark.parametrize("bm", ["192", "128"])
+def test_gemm_bm192(dev, b_lay, mnk, bm, monkeypatch):
+    """192- and 128-row tiles of the v4 kernel (forced): ragged M / N, one tile, several persistent tiles per
+    block (M = 50000: 261 x 2 tiles on 256 CUs at 192 rows), one K-tile, KC x KC and KC x RC."""
+    monkeypatch.setenv("MAECLIP_GEMM_BM", bm)
     M, N, Kd = mnk
     A = _rand((M, Kd), torch.bfloat16, dev, seed=1)
     B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, seed=2)
@@ -104,14 +105,17 @@ def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
     _sk_counters_zero()
 
 
-@pytest.mark.parametrize("mode", ["split2_192", "split2_192_lead0"])
+@pytest.mark.parametrize("mode", ["split2_192", "split2_192_lead0", "bm128"])
 def test_gemm_stream_k_epilogues(dev, mode, monkeypatch):
     """Every fused epilogue behind the split fix-up (the last block runs it
     on the summed tile): bias + GELU / GELU' (aux_out), fp32 residual, column
     sums, dGELU, mul-aux + residual; M = 3000 x N = 768 (36 / 48 tiles, every
     tile cut) at K = 1024."""
-    monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
-    monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+    if mode == "bm128":   # the 128-row tile's epilogues (no split)
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "128")
+    else:
+        monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
+        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
     if "_lead" in mode:
         monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
     M, N, Kd = 3000, 768, 1024

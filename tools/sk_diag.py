@@ -58,7 +58,8 @@ def time_one(fn, reps=10):
 
 
 MODES = {"dp": {"MAECLIP_GEMM_SK": "0"}, "auto": {}, "dp256": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "256"},
-         "dp192": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "192"}}
+         "dp192": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "192"},
+         "dp128": {"MAECLIP_GEMM_SK": "0", "MAECLIP_GEMM_BM": "128"}}
 for d in (0, 2, 4, 6, 8):
     MODES[f"split2_192_d{d}"] = {"MAECLIP_GEMM_SPLIT": "2", "MAECLIP_GEMM_BM": "192", "MAECLIP_GEMM_SPLIT_D": str(d)}
 if os.environ.get("SKMODES"):
@@ -66,7 +67,7 @@ if os.environ.get("SKMODES"):
 
 
 def setmode(v):
-    for k in ("MAECLIP_GEMM_SK", "MAECLIP_GEMM_BM", "MAECLIP_GEMM_SPLIT", "MAECLIP_GEMM_SPLIT_D"):
+    for k in ("MAECLIP_GEMM_SK", "MAECLIP_GEMM_BM", "MAECLIP_GEMM_SPLIT", "MAECLIP_GEMM_SPLIT_D", "MAECLIP_GEMM_BM128"):
         os.environ.pop(k, None)
     if isinstance(v, str):
         v = {"MAECLIP_GEMM_SK": v}
