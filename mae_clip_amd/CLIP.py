@@ -117,7 +117,7 @@ class CLIPModel(nn.Module):
         if use_side:
             side = Fn.side_stream(img.device)
             side.wait_stream(main)
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(side), K.gemm_split_scope(bool(CFG.text_gemm_split)):
                 text_features = self.text_encoder(batch["input_ids"], batch["attention_mask"], seed=seed + 17,
                                                   dtype=dtype, step_ptr=sc)
         cache = self._weight_cache()

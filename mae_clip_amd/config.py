@@ -77,4 +77,5 @@ dp_encoder_chunk = (1, 2, 3, 6)
 dp_decoder_chunk = 4       # data parallel: decoder blocks per autograd Function (overlapped by the encoder backward)
 dp_grad_dtype = "fp32"     # data parallel gradient all-reduce: "fp32" (exact) or "bf16" (opt-in, half the bytes)
 stack_microbatches = 2     # bf16 stacks: samples cut into this many micro-batches, each chain on its own stream
+text_gemm_split = __import__("os").environ.get("MAECLIP_TEXT_SPLIT", "0") == "1"  # frozen text tower's GEMMs on the split plan (MAECLIP_GEMM_SK=1 scope; A/B knob)
 wgrad_grouped = True       # all weight gradients of a stack in one grouped GEMM launch (maeclip_wgrad_grouped)

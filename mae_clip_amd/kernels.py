@@ -67,6 +67,31 @@ def alias_stream(capture_stream, replay_stream):
         _STREAM_ALIAS[capture_stream] = replay_stream
 
 
+class gemm_split_scope:
+    """Launches issued inside the scope may take maeclip_gemm's split plan
+    (MAECLIP_GEMM_SK=1, read per launch by the library); restores the previous
+    setting on exit. Host-thread scoped: the library reads the environment."""
+
+    def __init__(self, enabled=True):
+        self.enabled, self.prev = enabled, None
+
+    def __enter__(self):
+        if self.enabled:
+            import os
+            self.prev = os.environ.get("MAECLIP_GEMM_SK")
+            os.environ["MAECLIP_GEMM_SK"] = "1"
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            import os
+            if self.prev is None:
+                os.environ.pop("MAECLIP_GEMM_SK", None)
+            else:
+                os.environ["MAECLIP_GEMM_SK"] = self.prev
+        return False
+
+
 def _stream_scratch(device, nbytes):
     """Per-(device, stream) scratch kept for the process (maeclip_gemm's
     stream-K counters and partial tiles): launches on one stream run in order
