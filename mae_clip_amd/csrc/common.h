@@ -163,6 +163,72 @@ __device__ __forceinline__ void gelu_pair2(mc_f32x2 x, mc_f32x2& y, mc_f32x2& dy
   y = x * cdf;
   dy = __builtin_elementwise_fma(x * e, (mc_f32x2){0.39894228040143268f, 0.39894228040143268f}, cdf);
 }
+// The GEMM epilogue's form of the same pair over NP value pairs at once, each
+// step applied to every pair before the next (the dependent packed ops of one
+// pair would otherwise stand back to back and take a wait state each), with
+// the constants folded:
+//   t   = 1 / (1 + (p / sqrt2) |x|)                 (|x| as an fma source modifier)
+//   phi = 2^(x (x (-log2(e) / 2)) + log2(1 / sqrt(2 pi)))  = exp(-x^2/2) / sqrt(2 pi)
+//   ht  = t P'(t) phi,  P' = sqrt(pi / 2) P          = 0.5 erfc(|x| / sqrt2)
+//   cdf = x < 0 ? ht : 1 - ht                       (sign mask + bit select, no compare)
+//   y = x cdf,  dy = x phi + cdf
+// The same approximation as gelu_pair; the result differs from it only by the
+// rounding of the folded constants (a few f32 ulp, far below the bf16 output).
+template <int NP>
+__device__ __forceinline__ void gelu_pairs(const mc_f32x2 (&x)[NP], mc_f32x2 (&y)[NP], mc_f32x2 (&dy)[NP]) {
+  constexpr float KD = 0.3275911f * 0.70710678118654752f;
+  constexpr float KE = -0.72134752044448170f;          // -log2(e) / 2
+  constexpr float KC = -1.3257480647361593f;           // log2(1 / sqrt(2 pi))
+  constexpr float S = 1.2533141373155003f;             // sqrt(pi / 2) = 0.5 sqrt(2 pi)
+  mc_f32x2 t[NP], e[NP], p[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) t[i][h] = fmaf(fabsf(x[i][h]), KD, 1.0f);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) e[i] = x[i] * KE;
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) t[i][h] = __builtin_amdgcn_rcpf(t[i][h]);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) e[i] = __builtin_elementwise_fma(e[i], x[i], (mc_f32x2){KC, KC});
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) e[i][h] = __builtin_amdgcn_exp2f(e[i][h]);
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    p[i] = __builtin_elementwise_fma(t[i], (mc_f32x2){1.061405429f * S, 1.061405429f * S},
+                                     (mc_f32x2){-1.453152027f * S, -1.453152027f * S});
+#pragma unroll
+  for (int i = 0; i < NP; ++i) p[i] = __builtin_elementwise_fma(t[i], p[i], (mc_f32x2){1.421413741f * S, 1.421413741f * S});
+#pragma unroll
+  for (int i = 0; i < NP; ++i) p[i] = __builtin_elementwise_fma(t[i], p[i], (mc_f32x2){-0.284496736f * S, -0.284496736f * S});
+#pragma unroll
+  for (int i = 0; i < NP; ++i) p[i] = __builtin_elementwise_fma(t[i], p[i], (mc_f32x2){0.254829592f * S, 0.254829592f * S});
+#pragma unroll
+  for (int i = 0; i < NP; ++i) p[i] = p[i] * t[i];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) p[i] = p[i] * e[i];                      // ht
+#pragma unroll
+  for (int i = 0; i < NP; ++i) t[i] = (mc_f32x2){1.0f, 1.0f} - p[i];      // 1 - ht
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // all ones for x < 0; one v_bfi_b32 (written out: as C the select
+      // becomes a compare into an SGPR pair + v_cndmask, with wait states)
+      const int m = __float_as_int(x[i][h]) >> 31;
+      float r;
+      asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(p[i][h]), "v"(t[i][h]));
+      t[i][h] = r;
+    }
+#pragma unroll
+  for (int i = 0; i < NP; ++i) y[i] = x[i] * t[i];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) dy[i] = __builtin_elementwise_fma(x[i], e[i], t[i]);
+}
 // gelu and gelu' of the 4 lanes of v: v <- gelu(v), returns gelu'(v)
 __device__ __forceinline__ v4f gelu4_inplace(v4f& v) {
   v4f d;

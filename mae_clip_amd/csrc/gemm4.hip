@@ -411,15 +411,21 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       const bool ok = m < M && nok;
       if (EPI == EPI_GELU || EPI == EPI_GELU_D) {
         float d[VPL];   // GELU: aux_out <- pre-activation; GELU_D: aux_out <- gelu'(pre)
+        mc_f32x2 xv[VPL / 2], yv[VPL / 2], dv[VPL / 2];   // value pairs: packed f32 math
 #pragma unroll
-        for (int v = 0; v < VPL; v += 2) {   // value pairs: packed f32 math (gelu_pair2)
-          mc_f32x2 y, dy;
-          const mc_f32x2 xv = {x[v], x[v + 1]};
-          gelu_pair2(xv, y, dy);
-          d[v] = EPI == EPI_GELU_D ? dy[0] : x[v];
-          d[v + 1] = EPI == EPI_GELU_D ? dy[1] : x[v + 1];
-          x[v] = y[0];
-          x[v + 1] = y[1];
+        for (int v = 0; v < VPL; v += 2) xv[v / 2] = mc_f32x2{x[v], x[v + 1]};
+#ifdef GEMM4_OLD_GELU   // A/B builds only: the round-5 first form, pair by pair
+#pragma unroll
+        for (int v = 0; v < VPL / 2; ++v) gelu_pair2(xv[v], yv[v], dv[v]);
+#else
+        gelu_pairs<VPL / 2>(xv, yv, dv);
+#endif
+#pragma unroll
+        for (int v = 0; v < VPL; v += 2) {
+          d[v] = EPI == EPI_GELU_D ? dv[v / 2][0] : x[v];
+          d[v + 1] = EPI == EPI_GELU_D ? dv[v / 2][1] : x[v + 1];
+          x[v] = yv[v / 2][0];
+          x[v + 1] = yv[v / 2][1];
         }
         if (args.aux_out && ok) {
           bf16_t* ap = (bf16_t*)args.aux_out + off + (int64_t)m * args.ldaux + n;
@@ -1235,7 +1241,10 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
 template <int LA, int LB, typename OutT>
 int epi4(const maeclip_gemm_args& a, hipStream_t s) {
 #ifdef GEMM4_DEV_SUBSET   // register / ISA inspection builds only: one epilogue
-  return launch4<LA, LB, OutT, EPI_NONE>(a, s);
+#ifndef GEMM4_DEV_EPI
+#define GEMM4_DEV_EPI EPI_NONE
+#endif
+  return launch4<LA, LB, OutT, GEMM4_DEV_EPI>(a, s);
 #else
   switch (a.epilogue) {
     case EPI_NONE: return launch4<LA, LB, OutT, EPI_NONE>(a, s);
