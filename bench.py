@@ -203,8 +203,9 @@ def pmc_traffic(key):
     """HBM bytes per launch of GEMM shape `key` from the committed rocprofv3 PMC
     summaries (profiles/*/traffic_*.json, written by tools/pmc_traffic.sh:
     FETCH_SIZE x 2 + WRITE_SIZE, separate passes, MI355X_MICROARCH.md §HBM).
-    PMC counters cannot be read inside a timed run, so the newest matching file
-    is reported with its path; None when no summary covers the shape."""
+    PMC counters cannot be read inside a timed run, so the matching file of the
+    newest round directory (profiles/rNN, then the file name) is reported with
+    its path; None when no summary covers the shape."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json"))):
@@ -212,8 +213,8 @@ def pmc_traffic(key):
             r = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if r.get("shape", "").split(">")[0] == key.split(">")[0] and (best is None or os.path.getmtime(f) >= os.path.getmtime(best[0])):
-            best = (f, r)
+        if r.get("shape", "").split(">")[0] == key.split(">")[0]:
+            best = (f, r)   # sorted paths: a later round's file wins
     if best is None:
         return None, None
     return best[1]["hbm_bytes"], os.path.relpath(best[0], ROOT)

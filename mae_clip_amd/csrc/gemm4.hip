@@ -39,6 +39,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ int swz_rc(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
 
+#ifndef GEMM4_EPI_PF_AUX
+#define GEMM4_EPI_PF_AUX 2
+#endif
 #ifndef GEMM4_EPI_PF
 #define GEMM4_EPI_PF 2
 #endif
@@ -358,29 +361,40 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       csc[v + r] = sv[r] * alpha;
     }
   }
-  // aux / residual of chunk c + PF - 1 issued before chunk c is finished
+  // aux / residual of chunk c + PF - 1 issued before chunk c is finished;
+  // the aux ring (8 VGPRs a chunk) may run deeper than the residual one
+  // (16 / 32 VGPRs a chunk)
   constexpr int PF = GEMM4_EPI_PF;
+  constexpr int PFA = LOAD_AUX ? GEMM4_EPI_PF_AUX : 1;
   typedef unsigned int auxv_t __attribute__((ext_vector_type(L8 ? 4 : 2)));
-  auxv_t ax[PF][NQ];
+  auxv_t ax[PFA][NQ];
   v4f rs[PF][NQ][VPL / 4];
-  auto load_chunk = [&](int c, int buf) {
+  auto load_aux = [&](int c) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int m = min(rbase + 16 * c + RPI * q, M - 1);
-      if (LOAD_AUX) ax[buf][q] = NT_LD((const auxv_t*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + nc));
-      if (LOAD_RES && has_res) {
-        const float* rp = args.resid + off + (int64_t)m * args.ldr + nc;
+      ax[c % PFA][q] = NT_LD((const auxv_t*)((const bf16_t*)args.aux + off + (int64_t)m * args.ldaux + nc));
+    }
+  };
+  auto load_res = [&](int c) {
 #pragma unroll
-        for (int v = 0; v < VPL / 4; ++v) rs[buf][q][v] = NT_LD((const v4f*)(rp + 4 * v));
-      }
+    for (int q = 0; q < NQ; ++q) {
+      const int m = min(rbase + 16 * c + RPI * q, M - 1);
+      const float* rp = args.resid + off + (int64_t)m * args.ldr + nc;
+#pragma unroll
+      for (int v = 0; v < VPL / 4; ++v) rs[c % PF][q][v] = NT_LD((const v4f*)(rp + 4 * v));
     }
   };
   float csum[VPL];
 #pragma unroll
   for (int v = 0; v < VPL; ++v) csum[v] = 0.f;
-  if (LOAD_AUX || LOAD_RES) {
+  if constexpr (LOAD_AUX) {
 #pragma unroll
-    for (int c = 0; c < PF - 1; ++c) load_chunk(c, c);
+    for (int c = 0; c < PFA - 1; ++c) load_aux(c);
+  }
+  if (LOAD_RES && has_res) {
+#pragma unroll
+    for (int c = 0; c < PF - 1; ++c) load_res(c);
   }
   // fragment -> scratch offsets of this lane (row lane & 15; units 8 ni + 4 (g & 1) + 2 (g >> 1) + e)
   int wo[4];
@@ -390,7 +404,8 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
     for (int e = 0; e < 2; ++e) wo[2 * ni + e] = scr_off(lane & 15, 8 * ni + 4 * (g & 1) + 2 * (g >> 1) + e);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    if ((LOAD_AUX || LOAD_RES) && c + PF - 1 < NCH) load_chunk(c + PF - 1, (c + PF - 1) % PF);
+    if (LOAD_AUX && c + PFA - 1 < NCH) load_aux(c + PFA - 1);
+    if (LOAD_RES && has_res && c + PF - 1 < NCH) load_res(c + PF - 1);
     __builtin_amdgcn_sched_barrier(0);   // keep chunk c+1's loads ahead of chunk c's stores
 #pragma unroll
     for (int j = 0; j < 4; ++j) *(v4f*)(scr + wo[j]) = acc[c][j];
@@ -440,7 +455,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
         }
       }
       if (LOAD_AUX) {
-        const auxv_t pk = ax[c % PF][q];
+        const auxv_t pk = ax[c % PFA][q];
 #pragma unroll
         for (int r = 0; r < VPL / 2; ++r) {
           const float a0 = __uint_as_float(pk[r] << 16), a1 = __uint_as_float(pk[r] & 0xffff0000u);
