@@ -282,11 +282,26 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t bh, int q, 
 // ============================================================== forward
 // max over the four 16-lane rows (the lanes l, l^16, l^32, l^48 of a query):
 // two permlane swaps (VALU) instead of two ds_bpermute round trips
+// (ATTN_RAWMAX: a plain v_max_f32 of the two halves -- fmaxf would first
+// canonicalise each permlane result, two more VALU ops per swap; the scores
+// are never signalling NaNs)
+#ifndef ATTN_RAWMAX
+#define ATTN_RAWMAX 0   // measured: the asm pins the schedule (C4 decoder fwd 255 -> 280 us)
+#endif
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+#if ATTN_RAWMAX
+  float r;
+  asm volatile("v_max_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmaxf(a, b);
+#endif
+}
 __device__ __forceinline__ float max4rows(float x) {
   const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  x = vmax_raw(__uint_as_float(p[0]), __uint_as_float(p[1]));
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax_raw(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float sum4rows(float x) {
   const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -304,26 +319,45 @@ struct FwdDrop {
 // One 64-key chunk of a 16-query tile with its shape fixed at compile time, so
 // the body is straight-line code the scheduler can interleave (the runtime
 // per-32-key / mask / dropout branches of a generic body split it into ~30
-// basic blocks with an MFMA or a few VALU ops each). NH: 32-key halves that
-// hold real keys (1 only for the tail chunk of n = 197: keys 192..223);
-// MASKED: add the key bias (padding keys, DistilBERT's key mask) -- the scale
-// c > 0 then rides in the bias fma, otherwise in the exponent's fma and the
-// running max is taken on the raw scores.
+// basic blocks with an MFMA or a few VALU ops each). NT: 16-key S tiles that
+// hold real keys (4 for a whole chunk; the tail chunk of n = 197, keys
+// 192..196, runs one tile instead of two -- its PV product takes a zero
+// second half); MASKED: add the key bias (padding keys, DistilBERT's key mask)
+// -- the scale c > 0 then rides in the bias fma, otherwise in the exponent's
+// fma and the running max is taken on the raw scores.
 // bf16 without dropout: the row sum of P comes out of the MFMA as a
 // 17th..32nd "V column" of ones (lsum accumulator `ol`, every element the
 // lane's query's sum of the bf16 P the PV product uses) instead of 16 VALU
 // adds per chunk -- the kernel is VALU-bound at HD 32, the MFMA pipe is not;
 // lsum is then the exact weight sum of O = sum P V (both over bf16(P)).
 // With dropout the normalisation needs the sum BEFORE the mask: VALU adds.
-template <typename T, int HD, int NH, bool MASKED, bool DROP>
+// bf16 rescales lazily: the running max m only moves (alpha exp + the O / lsum
+// multiplies) when some query of the wave sees a chunk max more than LAZY_TH
+// (log2 units) above it; otherwise P = exp2(s' - m) <= 2^LAZY_TH. bf16(P) has
+// the same relative rounding at any exponent, O and lsum accumulate in f32,
+// and lse = m + log2(lsum) holds for any m, so only the f32 roundings of the
+// final O / lsum change. Wave-uniform branch (ballot), taken on the first
+// chunk (m = -1e30) and then rarely.
+#ifndef LAZY_TH
+#define LAZY_TH 8.0f
+#endif
+#ifndef ATTN_PKFMA
+#define ATTN_PKFMA 0   // measured: neutral to -3 % (dec 75 -> 77-80 us)
+#endif
+#ifndef ATTN_LAZY
+#define ATTN_LAZY 0   // measured slower (the branch splits the chunk body): opt-in
+#endif
+template <typename T, int HD, int NT, bool MASKED, bool DROP>
 __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, const float* kmask, int kc,
                                           const RowFrag<T, HD> (&qf)[HD / 32], float c, float& m, float& lsum,
                                           v4f (&o)[HD / 16], v4f& ol, int lane, const FwdDrop& dr, int q) {
-  constexpr bool MSUM = std::is_same<T, bf16_t>::value && !DROP;
+  constexpr bool BF = std::is_same<T, bf16_t>::value;
+  constexpr bool MSUM = BF && !DROP;
+  constexpr int NP = (NT + 1) / 2;   // 32-key halves of the PV product
   const int g = lane >> 4;
-  v4f s[2 * NH];
+  v4f s[2 * NP];
 #pragma unroll
-  for (int t = 0; t < 2 * NH; ++t) {
+  for (int t = 0; t < NT; ++t) {
     s[t] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < HD / 32; ++ks) {
@@ -335,7 +369,7 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
   float mloc = NEG_BIG;
   if (MASKED) {
 #pragma unroll
-    for (int t = 0; t < 2 * NH; ++t) {
+    for (int t = 0; t < NT; ++t) {
       const v4f km = *(const v4f*)(kmask + kc + 16 * t + 4 * g);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -345,35 +379,52 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
     }
   } else {
 #pragma unroll
-    for (int t = 0; t < 2 * NH; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) mloc = fmaxf(mloc, s[t][i]);
     mloc *= c;
   }
   mloc = max4rows(mloc);
-  const float mnew = fmaxf(m, mloc);
-  const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-  const float cc = MASKED ? 1.f : c, nm = -mnew;
+  float lsc = 1.f;
+  bool resc = true;
+  if (BF && ATTN_LAZY) resc = __builtin_amdgcn_ballot_w64(mloc > m + LAZY_TH) != 0;
+  if (resc) {
+    const float mnew = fmaxf(m, mloc);
+    lsc = __builtin_amdgcn_exp2f(m - mnew);
+    if (MSUM) ol[0] *= lsc;   // only element 0 is read back
+#pragma unroll
+    for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= lsc;
+    m = mnew;
+  }
+  const float cc = MASKED ? 1.f : c, nm = -m;
   float lp = 0.f;
 #pragma unroll
-  for (int t = 0; t < 2 * NH; ++t)
+  for (int t = 0; t < NT; ++t) {
+#if ATTN_PKFMA   // exponent arguments of a value pair in one v_pk_fma_f32 (A/B builds)
+    if (MSUM) {
+      typedef float f2_t __attribute__((ext_vector_type(2)));
+      const f2_t c2 = {cc, cc}, n2 = {nm, nm};
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const f2_t e = __builtin_elementwise_fma(f2_t{s[t][i], s[t][i + 1]}, c2, n2);
+        s[t][i] = __builtin_amdgcn_exp2f(e[0]);
+        s[t][i + 1] = __builtin_amdgcn_exp2f(e[1]);
+      }
+      continue;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], cc, nm));
       if (!MSUM) lp += p;
       s[t][i] = p;
     }
-  if (MSUM) {
-    ol[0] *= alpha;   // only element 0 is read back
-  } else {
-    lsum = fmaf(lsum, alpha, lp);
   }
-#pragma unroll
-  for (int dt = 0; dt < HD / 16; ++dt) o[dt] *= alpha;
-  m = mnew;
+  if (NT & 1) s[NT] = v4f{0.f, 0.f, 0.f, 0.f};
+  if (!MSUM) lsum = fmaf(lsum, lsc, lp);
   if (DROP) {
 #pragma unroll
-    for (int t = 0; t < 2 * NH; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = kc + 16 * t + 4 * g + i;
@@ -381,7 +432,7 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
       }
   }
 #pragma unroll
-  for (int s2 = 0; s2 < NH; ++s2) {
+  for (int s2 = 0; s2 < NP; ++s2) {
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt)
       o[dt] = mma_rowsum<T, HD>(Vimg, kc + 32 * s2, 16 * dt, s[2 * s2], s[2 * s2 + 1], o[dt], lane);
@@ -448,10 +499,13 @@ attn_fwd_kernel(const maeclip_attn_args a) {
 
     int kc = 0;
     for (; kc < 64 * nfull; kc += 64)
-      fwd_chunk<T, HD, 2, false, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
+      fwd_chunk<T, HD, 4, false, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
     for (; kc < npad; kc += 64) {
-      // 32-key halves of this chunk that hold real keys (wave-uniform)
-      if (n - kc > 32) fwd_chunk<T, HD, 2, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
+      // 16-key tiles of this chunk that hold real keys (wave-uniform; n > kc)
+      const int rem = n - kc;
+      if (rem > 48) fwd_chunk<T, HD, 4, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
+      else if (rem > 32) fwd_chunk<T, HD, 3, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
+      else if (rem > 16) fwd_chunk<T, HD, 2, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
       else fwd_chunk<T, HD, 1, true, DROP>(Kimg, Vimg, kmask, kc, qf, c, m, lsum, o, ol, lane, dr, q);
     }
     // the MFMA row sum (bf16, no dropout) is whole in every lane of the query
