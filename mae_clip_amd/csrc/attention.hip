@@ -341,6 +341,9 @@ struct FwdDrop {
 #ifndef LAZY_TH
 #define LAZY_TH 8.0f
 #endif
+#ifndef ATTN_BWD_FLAGS
+#define ATTN_BWD_FLAGS 1
+#endif
 #ifndef ATTN_PKFMA
 #define ATTN_PKFMA 0   // measured: neutral to -3 % (dec 75 -> 77-80 us)
 #endif
@@ -862,6 +865,8 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
   float* csv = (float*)(dst + NW * 2048);         // [4 NW][HD] v-bias partials (one row per 16-lane row)
   float* csq = csv + 4 * NW * HD;                 // [4 NW][HD] q-bias partials
   char* myds = dst + wave * 2048;
+  int* rflag = (int*)(csq + 4 * NW * HD);         // [NW] rounds whose dQ update wave w has finished
+  if (threadIdx.x < NW) rflag[threadIdx.x] = 0;   // published by the prologue's barrier
   ASTAMP(0);
 
   const int HH = H * HD;
@@ -1063,7 +1068,20 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
         dk[kt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT[dt], ps, dk[kt][dt], 0, 0, 0);
       }
     }
-    // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] for this wave's 32 keys
+    // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q] for this wave's 32 keys.
+    // ATTN_BWD_FLAGS: instead of a workgroup barrier per round, wave w waits
+    // only for the wave that added into this query chunk in the round before
+    // ((w + 1) mod NC, one LDS flag); every other phase of the round depends on
+    // no other wave, so the waves drift apart by at most a round each and their
+    // exp / MFMA / LDS phases interleave. The order of the adds per chunk (and
+    // so the result) is the barrier schedule's.
+#if ATTN_BWD_FLAGS
+    if (r > 0) {
+      const int src = wave + 1 == NW ? 0 : wave + 1;
+      while (__hip_atomic_load(&rflag[src], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < r)
+        __builtin_amdgcn_s_sleep(1);
+    }
+#endif
     char* dQr = dQi + q0 * DQB;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1076,7 +1094,11 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
         *pq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kT[dt], bds, *pq, 0, 0, 0);
       }
     }
+#if ATTN_BWD_FLAGS
+    __hip_atomic_store(&rflag[wave], r + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
     __syncthreads();
+#endif
   }
   ASTAMP(2);
 
@@ -1094,6 +1116,9 @@ attn_bwd_diag_kernel(const maeclip_attn_args a) {
     }
   }
   ASTAMP(3);
+#if ATTN_BWD_FLAGS
+  __syncthreads();   // every wave's last dQ update is in
+#endif
   // dQ rows: thread -> (row, 4 columns); q-bias partial per (row group, column)
   float cq[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int C4N = HD / 4;   // 16-B chunks per dQ row
@@ -1341,7 +1366,7 @@ int run_rows(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
 template <int HD> size_t bwd_diag_lds(int n) {
   const int npad = (n + 31) & ~31, nw = npad / 32;
   return (size_t)2 * npad * Img<bf16_t, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)npad * 4 * HD +
-         (size_t)nw * 2048 + (size_t)8 * nw * HD * 4;
+         (size_t)nw * 2048 + (size_t)8 * nw * HD * 4 + (size_t)nw * 4;
 }
 
 template <typename T, int HD> size_t fwd_lds(int n) {
