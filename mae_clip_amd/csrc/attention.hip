@@ -1448,15 +1448,17 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
   dim3 grid((unsigned)(a.B * a.H));
   if constexpr (std::is_same<T, bf16_t>::value) {
     // one-pass diagonal backward: the default at HD 32 up to npad 256
-    // (MAECLIP_ATTN_DIAG=0 turns it off); opt-in (MAECLIP_ATTN_DIAG=1) at HD 64
-    // while its LDS fits (npad <= 224). Measured slower there (C1 encoder 323
-    // vs 280 us, C4 encoder 157 vs 123, C2 encoder 49 vs 46;
-    // profiles/r03/attn_diag64_ab.txt): the 56 KB f32 dQ image leaves one
-    // workgroup per CU, whose ~140 KB prologue then has nothing to overlap with.
+    // (MAECLIP_ATTN_DIAG=0 turns it off). HD 64 (LDS fits up to npad 224): the
+    // 56 KB f32 dQ image leaves one workgroup per CU, whose ~140 KB prologue
+    // has nothing to overlap with -- slower everywhere with a barrier per
+    // round (profiles/r03/attn_diag64_ab.txt); with the per-wave round flags
+    // it wins at the long rows only (C1 encoder n = 197: 299 -> 289 us; C2
+    // encoder n = 50: 52 -> 55; C4 n = 145 even; profiles/r05/attn_diag64_ab_r5ag.txt),
+    // so it is the default for npad >= 192 (MAECLIP_ATTN_DIAG=1 / 0 forces it on / off).
     const char* e = getenv("MAECLIP_ATTN_DIAG");
     const int npad = (a.n + 31) & ~31;
     const size_t ld = bwd_diag_lds<HD>(a.n);
-    const bool want = HD == 32 ? !(e && *e == '0') : (e && *e == '1');
+    const bool want = HD == 32 ? !(e && *e == '0') : (e && *e ? *e == '1' : npad >= 192);
     if (bwd && npad <= 256 && ld <= 163840 && want && !a.key_mask) {
       if (ld > 65536)
         (void)hipFuncSetAttribute((const void*)attn_bwd_diag_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize,
