@@ -558,8 +558,10 @@ __device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane
 // OCC > 1 asks the compiler for that many resident 8-wave workgroups per CU
 // (register budget 512 / (2 OCC)); used with TWO_ at HD = 32, where the
 // two-image LDS footprint would allow three.
-template <typename T, int HD, bool SDS, bool TWO_ = false, int OCC = 1>
-__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(2 * OCC)))
+// WG = 16: up to 16 waves in the one workgroup a CU holds (the C4 decoder,
+// n = 577: 37 tiles, at most 3 per wave instead of 5; register budget 128).
+template <typename T, int HD, bool SDS, bool TWO_ = false, int OCC = 1, int WG = MAXW>
+__global__ void __launch_bounds__(WG * 64) __attribute__((amdgpu_waves_per_eu(WG > MAXW ? 4 : 2 * OCC)))
 attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
@@ -1379,12 +1381,12 @@ template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
-template <typename T, int HD, bool SDS, bool TWO = false, int OCC = 1>
+template <typename T, int HD, bool SDS, bool TWO = false, int OCC = 1, int WG = MAXW>
 void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO, OCC>,
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO, OCC, WG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO, OCC>), grid, dim3(nthreads), lds, s, a);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO, OCC, WG>), grid, dim3(nthreads), lds, s, a);
 }
 
 // resident workgroups per CU of a bwd variant (registers, waves and LDS)
@@ -1466,6 +1468,24 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
       hipLaunchKernelGGL(attn_bwd_diag_kernel<HD>, grid, dim3(2 * npad), ld, s, a);
       MC_CHECK_LAUNCH("maeclip_attn_bwd(diag)");
       return 0;
+    }
+  }
+  if constexpr (std::is_same<T, bf16_t>::value) {
+    // bf16 rows beyond the diagonal kernel with more 16-row tiles than MAXW
+    // waves: the two-image layout with up to 16 waves, default at HD 32 (C4
+    // decoder n = 577: 604 -> 555 us; at HD 64 the C4 encoder, n = 145, loses:
+    // 147 -> 168; profiles/r05/attn_bw16_ab_r5ah.txt). MAECLIP_ATTN_BW16=1 / 0
+    // forces it on / off.
+    const char* e16 = getenv("MAECLIP_ATTN_BW16");
+    const bool bw16 = e16 && *e16 ? *e16 != '0' : HD == 32;
+    if (bwd && tiles > MAXW && bw16) {
+      const int nw16 = tiles < 16 ? tiles : 16;
+      const size_t lds16 = bwd_lds<T, HD>(a.n, nw16, true);
+      if (lds16 <= 163840) {
+        launch_bwd<T, HD, false, true, 1, 16>(a, grid, 64 * nw16, lds16, s);
+        MC_CHECK_LAUNCH("maeclip_attn_bwd(16 waves)");
+        return 0;
+      }
     }
   }
   if (bwd) {

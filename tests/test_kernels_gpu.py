@@ -218,7 +218,7 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
-@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag", "rows"])
+@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag", "bw16", "rows"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
                                    (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32), (1, 577, 2, 32),
@@ -233,7 +233,9 @@ def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     diagonal schedule with dQ accumulated in LDS ("diag": bf16, n <= 256 at
     hd = 32, n <= 224 at hd = 64; the default there). fp32 beyond its LDS images (n = 577, the C4
     decoder) streams 64-row blocks through LDS ("rows"; forced here at every
-    shape, picked by itself at n = 577 in "four")."""
+    shape, picked by itself at n = 577 in "four"); "bw16": the two-image
+    layout with up to 16 waves (bf16, more than 8 16-row tiles; the default at
+    hd = 32 beyond the diagonal kernel, forced here at hd 64 too)."""
     B, n, H, hd = shape
     if dtype == torch.float32 and mode not in ("four", "rows"):
         pytest.skip("fp32 parity mode: MFMA kernel (two images) or the rows path")
@@ -243,6 +245,9 @@ def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
     if mode == "diag" and (dtype == torch.float32 or n > (256 if hd == 32 else 224)):
         pytest.skip("diagonal backward: bf16, n <= 256 at hd 32, n <= 224 at hd 64")
     monkeypatch.setenv("MAECLIP_ATTN_DIAG", "1" if mode == "diag" else "0")
+    if mode == "bw16" and (dtype == torch.float32 or n <= 128):
+        pytest.skip("16-wave backward: bf16 with more than 8 16-row tiles")
+    monkeypatch.setenv("MAECLIP_ATTN_BW16", "1" if mode == "bw16" else "0")
     monkeypatch.setenv("MAECLIP_ATTN_TWO", {"two": "1", "two3": "3"}.get(mode, "0"))
     if mode == "sds":
         # bf16 backward keeps dS in LDS for dQ instead of recomputing S/dP (opt-in)
