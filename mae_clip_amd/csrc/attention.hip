@@ -446,8 +446,13 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
   }
 }
 
-template <typename T, int HD, bool DROP>
-__global__ void __launch_bounds__(MAXW * 64) __attribute__((amdgpu_waves_per_eu(fwd_wpe<T, HD, DROP>())))
+// WG = 16: up to 16 waves when the K / V images leave room for one workgroup
+// per CU only (the C4 decoder, n = 577: 37 query tiles in 3 rounds of 13
+// waves instead of 5 rounds of 8)
+template <int A, int B> constexpr int cmax() { return A > B ? A : B; }
+template <typename T, int HD, bool DROP, int WG = MAXW>
+__global__ void __launch_bounds__(WG * 64)
+__attribute__((amdgpu_waves_per_eu(WG > MAXW ? cmax<fwd_wpe<T, HD, DROP>(), 4>() : fwd_wpe<T, HD, DROP>())))
 attn_fwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
@@ -1505,8 +1510,17 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     if (!sds && !two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
     auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true> : attn_fwd_kernel<T, HD, false>;
+    int nth = nthreads;
+    // one workgroup per CU by LDS and more tiles than MAXW waves: up to 16
+    // waves (MAECLIP_ATTN_FW16=0 turns it off)
+    const char* e16 = getenv("MAECLIP_ATTN_FW16");
+    if (tiles > MAXW && 2 * lds > 163840 && !(e16 && *e16 == '0')) {
+      const int r16 = (tiles + 15) / 16;
+      nth = 64 * ((tiles + r16 - 1) / r16);
+      kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true, 16> : attn_fwd_kernel<T, HD, false, 16>;
+    }
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, grid, dim3(nthreads), lds, s, a);
+    hipLaunchKernelGGL(kern, grid, dim3(nth), lds, s, a);
   }
   MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");
   return 0;
