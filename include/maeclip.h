@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 9
+#define MAECLIP_ABI_VERSION 10
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -221,7 +221,8 @@ typedef struct {
 int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* args, void* stream);
 
 /* bwd: dx(f32) = LN'(dy) + dres; dx_bf optional bf16 copy; partials
- * [maeclip_ln_bwd_partial_rows(M)][D] of dgamma, dbeta, colsum(dx).
+ * [maeclip_ln_bwd_partial_rows(M, D)][D] of dgamma, dbeta, colsum(dx) (ABI 10: the
+ * count depends on D -- up to 1024 workgroups at D <= 512, 512 above).
  * dres_pool (instead of dres, optional): the residual gradient is the
  * backward of timm's global_pool="avg" over pool_n tokens per sample, read
  * from dres_pool [M / pool_n][D]: row r gets dres_pool[r / pool_n] / (pool_n - 1)
@@ -253,7 +254,7 @@ typedef struct {
   int32_t q8_fmt;
 } maeclip_ln_bwd_args;
 int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* args, void* stream);
-int32_t maeclip_ln_bwd_partial_rows(int64_t M);
+int32_t maeclip_ln_bwd_partial_rows(int64_t M, int64_t D);
 
 /* ------------------------------------------------------------ reductions */
 /* out[n] (+)= scale * sum_p partial[p*N + n]  (fixed order -> deterministic);

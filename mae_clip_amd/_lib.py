@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -163,7 +163,7 @@ _SIGS = {
     "maeclip_attn_bwd": (c_i32, [C.POINTER(AttnArgs), c_vp]),
     "maeclip_ln_fwd": (c_i32, [C.POINTER(LnFwdArgs), c_vp]),
     "maeclip_ln_bwd": (c_i32, [C.POINTER(LnBwdArgs), c_vp]),
-    "maeclip_ln_bwd_partial_rows": (c_i32, [c_i64]),
+    "maeclip_ln_bwd_partial_rows": (c_i32, [c_i64, c_i64]),
     "maeclip_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_f32, c_vp, c_vp]),
     "maeclip_rows_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),

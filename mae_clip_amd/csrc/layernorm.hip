@@ -242,9 +242,21 @@ __global__ void __launch_bounds__(NTH) ln_bwd_kernel(const maeclip_ln_bwd_args a
   }
 }
 
-int ln_bwd_grid(int64_t M) {
-  int64_t g = (M + 3) / 4;
-  return (int)(g < 512 ? g : 512);
+// workgroups of the backward (each writes one partial row per output): 1024
+// at D <= 512 (the decoder: 72 -> 65 us alone at 50432 rows, 2 -> 4 waves per
+// SIMD), 512 above (D = 768 at 180 VGPRs holds 2 waves per SIMD anyway, and
+// 1024 measured slower: 31 -> 35 us; profiles/r05/ln_bwd_grid_ab_r5am.txt).
+// A next-row prefetch in the row loop measured slower alone (72 -> 83 us) and
+// neutral on the step (profiles/r05/ln_bwd_prefetch_ab_r5al.txt).
+#ifndef LN_BWD_GRID_CAP
+#define LN_BWD_GRID_CAP 512
+#endif
+#ifndef LN_BWD_GRID_CAP_NARROW
+#define LN_BWD_GRID_CAP_NARROW 1024
+#endif
+int ln_bwd_grid(int64_t M, int64_t D) {
+  const int64_t g = (M + 3) / 4, cap = D <= 512 ? LN_BWD_GRID_CAP_NARROW : LN_BWD_GRID_CAP;
+  return (int)(g < cap ? g : cap);
 }
 
 }  // namespace
@@ -273,7 +285,7 @@ extern "C" int32_t maeclip_ln_fwd(const maeclip_ln_fwd_args* a, void* stream) {
   return 0;
 }
 
-extern "C" int32_t maeclip_ln_bwd_partial_rows(int64_t M) { return ln_bwd_grid(M); }
+extern "C" int32_t maeclip_ln_bwd_partial_rows(int64_t M, int64_t D) { return ln_bwd_grid(M, D); }
 
 extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
   MC_CHECK_ARG(a && a->dy && a->x && a->mean && a->rstd && a->gamma && a->dx, "maeclip_ln_bwd: null pointer");
@@ -284,7 +296,7 @@ extern "C" int32_t maeclip_ln_bwd(const maeclip_ln_bwd_args* a, void* stream) {
   MC_CHECK_ARG(!a->dres_pool || (!a->dres && a->pool_n > 1 && a->M % a->pool_n == 0),
                "maeclip_ln_bwd: dres_pool needs pool_n > 1 dividing M (and no dres)");
   if (a->M == 0) return 0;
-  dim3 grid((unsigned)ln_bwd_grid(a->M));
+  dim3 grid((unsigned)ln_bwd_grid(a->M, a->D));
   hipStream_t s = (hipStream_t)stream;
   const int nc = (int)((a->D + 255) / 256);
   const int code = (a->dy_dtype == MAECLIP_BF16 ? 2 : 0) + (a->x_dtype == MAECLIP_BF16 ? 1 : 0);

@@ -457,7 +457,7 @@ class TransformerStackFn(torch.autograd.Function):
         e = lambda shape, dt=T: torch.empty(shape, device=dev, dtype=dt)
         f32 = torch.float32
         Ms = M // S
-        G = K.ln_bwd_partial_rows(Ms)          # LayerNorm partial rows per micro-batch
+        G = K.ln_bwd_partial_rows(Ms, D)       # LayerNorm partial rows per micro-batch
         GC = K.gemm_colsum_rows(M)              # GEMM column-sum partial rows (64-row groups)
         g = gy.reshape(M, D)
         if not g.is_contiguous():

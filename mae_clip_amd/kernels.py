@@ -441,8 +441,8 @@ def ln_fwd(x, gamma, beta, eps, out_dtype=None, res=None, in_dropout=0.0, out_dr
     return y, mean, rstd, yb, xs
 
 
-def ln_bwd_partial_rows(M: int) -> int:
-    return int(L.lib().maeclip_ln_bwd_partial_rows(M))
+def ln_bwd_partial_rows(M: int, D: int) -> int:
+    return int(L.lib().maeclip_ln_bwd_partial_rows(M, D))
 
 
 def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grads=True, want_colsum=False,
@@ -454,7 +454,7 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
     _dev(dy, x, mean, rstd, gamma, dres, dres_pool)
     M, D = x.shape
     dev = x.device
-    G = ln_bwd_partial_rows(M)
+    G = ln_bwd_partial_rows(M, D)
     e = lambda o, shape, dt: o if o is not None else torch.empty(shape, device=dev, dtype=dt)
     dx = e(dx_out, (M, D), torch.float32)
     dxb = e(dxb_out, (M, D), torch.bfloat16) if want_bf16 else None

@@ -21,7 +21,7 @@ def time_fn(fn, reps=30):
     return s.elapsed_time(e) / reps / 1e3
 
 
-for name, M, D in (("dec", 256 * 197, 512), ("enc", 256 * 50, 768)):
+for name, M, D in (("dec", 256 * 197, 512), ("enc", 256 * 50, 768), ("dec mb", 128 * 197, 512), ("enc mb", 128 * 50, 768)):
     x = torch.randn(M, D, device=dev)
     res = torch.randn(M, D, device=dev)
     g = torch.randn(D, device=dev)
