@@ -113,44 +113,12 @@ def parity_headline(device, precision="bf16", B=4):
 
 
 def train_curve_headline(device, precision="bf16", B=4, steps=5):
-    """The reference's train loop (main.py:54-66: forward, zero_grad, backward,
-    AdamW(lr 1e-3, wd 1e-3) step, main.py:101-103) for `steps` steps at the
-    metric's model shapes (ViT-B/16 @224, mask .75, 8x512 decoder, 6-layer
-    text) in TRAIN mode: the product at `precision` with its fused AdamW vs the
-    fp64 CPU oracle with torch.optim.AdamW, identical initial weights, batches
-    and MAE masks (both advance the mask step every training forward). Dropout
-    is set to 0 on both sides (the two RNG streams cannot match)."""
+    """The reference's train loop at the metric's model shapes vs the fp64 CPU
+    oracle (tests/helpers.py train_curve; asserted by
+    tests/test_model_gpu.py test_vitb_c2_train_curve_vs_oracle)."""
     sys.path.insert(0, ROOT)
-    from tests.helpers import build_pair, make_batch
-    from mae_clip_amd.optim import AdamW
-    kw = dict(model_name="vit_base_patch16_224", size=224, image_embedding=768, text_layers=6, mask_ratio=0.75,
-              decoder_embed_dim=512, decoder_depth=8, decoder_num_heads=16, dropout=0.0, text_dropout=0.0,
-              text_attention_dropout=0.0)
-    prod, ref = build_pair(precision, **kw)
-    for m in ref.modules():
-        if isinstance(m, torch.nn.Dropout):
-            m.p = 0.0
-    prod.train()
-    ref.train()
-    opt_p = AdamW([p for p in prod.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
-    opt_r = torch.optim.AdamW([p for p in ref.parameters() if p.requires_grad], lr=1e-3, weight_decay=1e-3)
-    rows = []
-    for k in range(steps):
-        b = make_batch(B, 224, seed=40 + k)
-        lp = prod({kk: v.to(device) for kk, v in b.items()})
-        opt_p.zero_grad()
-        lp.backward()
-        opt_p.step()
-        lr = ref(dict(b, image=b["image"].double()))
-        opt_r.zero_grad()
-        lr.backward()
-        opt_r.step()
-        lpv, lrv = lp.item(), lr.item()
-        rows.append({"step": k, "product": lpv, "oracle": lrv, "rel": abs(lpv - lrv) / max(1.0, abs(lrv))})
-    return {"precision": precision, "steps": steps, "batch": B, "worst_rel": max(r["rel"] for r in rows),
-            "last_rel": rows[-1]["rel"], "curve": rows,
-            "config": "C2 model shapes, train mode (dropout 0 both sides), AdamW lr 1e-3 wd 1e-3 (main.py:54-66, "
-                      ":101-103) vs the fp64 CPU oracle + torch.optim.AdamW"}
+    from tests.helpers import train_curve
+    return train_curve(device, precision, B, steps)
 
 
 def cpu_model_name():

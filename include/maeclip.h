@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MAECLIP_ABI_VERSION 10
+#define MAECLIP_ABI_VERSION 11
 #ifndef MAECLIP_F32
 #define MAECLIP_F32 0
 #define MAECLIP_BF16 1
@@ -37,6 +37,48 @@ int32_t maeclip_abi_version(void);
 const char* maeclip_last_error(void);
 /* number of gfx950 devices visible (0 when no GPU); does not create a context */
 int32_t maeclip_device_count(void);
+
+/* Plan options (A/B and test knobs of the kernels' launch planning). The
+ * library reads every MAECLIP_<name> environment variable ONCE, at the first
+ * call of any entry point below, into this table; launches read the table,
+ * never the environment. maeclip_set_option overrides one entry (value -1 =
+ * the built-in default). Defaults are the measured-fastest plans; no option
+ * changes results beyond the bf16 rounding of a different tile / split.
+ *   GEMM_BM          force a tile height of plain GEMMs (256 / 192 / 128; 0 auto)
+ *   GEMM_SK          1: the cost model may pick the aligned split plan (0 off)
+ *   GEMM_SPLIT       force a split of S slices (192-row tiles) where it fits
+ *   GEMM_SPLIT_D     slice 0's lead in K-tiles per other slice (default 4)
+ *   GEMM_SPLIT_MINK  the cost model's split only at K >= this (default 0)
+ *   GEMM_BM128       1: 128-row tiles enter the cost model (default 0)
+ *   GEMM_GRID        cap of the persistent GEMM grid (diagnostic; 0 = #CUs)
+ *   WG_SK            0: grouped weight gradients use uniform split-K slices
+ *                    instead of the stream-K remainder (default 1)
+ *   ATTN_TWO         bf16 attention backward layout: 0 four images, 1 two, 3
+ *                    two at 3 workgroups / CU (hd 32); -1 by occupancy
+ *   ATTN_ROWS        1: fp32 attention on the streaming rows path
+ *   ATTN_DIAG        diagonal backward (hd 32 on, hd 64 at npad >= 192); 0 / 1
+ *   ATTN_BW16        16-wave backward beyond MAXW tiles (default hd 32); 0 / 1
+ *   ATTN_FW16        16-wave forward when LDS leaves one workgroup (default 1) */
+enum {
+  MAECLIP_OPT_GEMM_BM = 0,
+  MAECLIP_OPT_GEMM_SK = 1,
+  MAECLIP_OPT_GEMM_SPLIT = 2,
+  MAECLIP_OPT_GEMM_SPLIT_D = 3,
+  MAECLIP_OPT_GEMM_SPLIT_MINK = 4,
+  MAECLIP_OPT_GEMM_BM128 = 5,
+  MAECLIP_OPT_GEMM_GRID = 6,
+  MAECLIP_OPT_WG_SK = 7,
+  MAECLIP_OPT_ATTN_TWO = 8,
+  MAECLIP_OPT_ATTN_ROWS = 9,
+  MAECLIP_OPT_ATTN_DIAG = 10,
+  MAECLIP_OPT_ATTN_BW16 = 11,
+  MAECLIP_OPT_ATTN_FW16 = 12,
+  MAECLIP_OPT_COUNT = 13
+};
+/* returns the previous value, or INT32_MIN for an unknown key */
+int32_t maeclip_set_option(int32_t key, int32_t value);
+/* current value (-1: default), INT32_MIN for an unknown key */
+int32_t maeclip_get_option(int32_t key);
 
 /* ------------------------------------------------------------------ GEMM
  * Replaces torch.nn.functional.linear (cuBLAS) for every nn.Linear on the

@@ -13,7 +13,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MAECLIP_LIB", os.path.join(_HERE, "libmaeclip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 10
+# plan options (include/maeclip.h MAECLIP_OPT_*), by name without the prefix
+OPTIONS = ("GEMM_BM", "GEMM_SK", "GEMM_SPLIT", "GEMM_SPLIT_D", "GEMM_SPLIT_MINK", "GEMM_BM128", "GEMM_GRID",
+           "WG_SK", "ATTN_TWO", "ATTN_ROWS", "ATTN_DIAG", "ATTN_BW16", "ATTN_FW16")
+ABI_VERSION = 11
 
 c_i32, c_i64, c_f32, c_u64, c_vp, c_sz = C.c_int32, C.c_int64, C.c_float, C.c_uint64, C.c_void_p, C.c_size_t
 
@@ -143,6 +146,8 @@ _SIGS = {
     "maeclip_abi_version": (c_i32, []),
     "maeclip_last_error": (C.c_char_p, []),
     "maeclip_device_count": (c_i32, []),
+    "maeclip_set_option": (c_i32, [c_i32, c_i32]),
+    "maeclip_get_option": (c_i32, [c_i32]),
     "maeclip_gemm": (c_i32, [C.POINTER(GemmArgs), c_vp]),
     "maeclip_gemm_colsum_rows": (c_i64, [c_i64]),
     "maeclip_gemm_workspace": (c_i64, [C.POINTER(GemmArgs)]),

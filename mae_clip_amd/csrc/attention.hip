@@ -45,10 +45,6 @@ template <typename T, int HD, bool DROP> constexpr int fwd_wpe() {
 #endif
 }
 
-bool getenv_flag(const char* name) {
-  const char* v = getenv(name);
-  return v && *v && *v != '0';
-}
 // Q / K / V / O / dO are read once per (sample, head): non-temporal loads, so
 // they do not evict what the next kernels reuse (ATTN_NT=0 turns it off)
 #ifndef ATTN_NT
@@ -537,30 +533,6 @@ attn_fwd_kernel(const maeclip_attn_args a) {
 }
 
 // ============================================================== backward
-// dS image (bf16 [npad keys][npad queries], phase 1 -> phase 2): 8-byte unit u
-// of row r lives at unit u ^ 4((r >> 2) & 1), so the eight rows a 32-lane half
-// of a ds_read_b64_tr_b16 touches fall on disjoint banks at npad = 224.
-__device__ __forceinline__ int dsimg_off(int row, int unit, int npad) {
-  return row * npad * 2 + ((unit ^ (((row >> 2) & 1) << 2)) << 3);
-}
-// B operand "dS^T" of the dQ product for keys kc..kc+31, queries q0 + (lane&15),
-// in the permuted k order of pack_p (element j <-> key kc + 16(j>>2) + 4g + (j&3))
-__device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane, int npad) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  v8s r;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = kc + 16 * h + 4 * g + q;
-    v4s t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(v4s, dsi + dsimg_off(row, (q0 >> 2) + p, npad)));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[4 * h + e] = t[e];
-  }
-  return r;
-}
-
-// SDS (bf16 only, when the n x n image fits beside Q, K, V, dO): phase 1
-// keeps dS in LDS and phase 2 reads it back instead of recomputing S, dP and
-// the exponentials (the exp/VALU work bounds the hd = 32 decoder layers).
 // TWO_ (bf16; always on for fp32): two [npad][HD] images in LDS instead of four --
 // phase 1 keeps Q, dO and reads each wave's K/V tile from HBM, phase 2 reloads
 // the slots with K, V. Chosen when it fits more workgroups per CU (C4: decoder
@@ -570,7 +542,7 @@ __device__ __forceinline__ v8s ds_frag(const char* dsi, int kc, int q0, int lane
 // two-image LDS footprint would allow three.
 // WG = 16: up to 16 waves in the one workgroup a CU holds (the C4 decoder,
 // n = 577: 37 tiles, at most 3 per wave instead of 5; register budget 128).
-template <typename T, int HD, bool SDS, bool TWO_ = false, int OCC = 1, int WG = MAXW>
+template <typename T, int HD, bool TWO_ = false, int OCC = 1, int WG = MAXW>
 __global__ void __launch_bounds__(WG * 64) __attribute__((amdgpu_waves_per_eu(WG > MAXW ? 4 : 2 * OCC)))
 attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -586,7 +558,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   // keeps Q, dO in LDS and reads each wave's K/V tile from HBM, phase 2
   // reloads the two slots with K, V and reads Q/dO tiles from HBM.
   constexpr bool TWO = TWO_ || !std::is_same<T, bf16_t>::value;
-  static_assert(!(SDS && TWO), "dS-in-LDS needs the four-image layout");
   const int img = npad * I::ROWB;
   char* Qi = smem;
   char* Di = smem + (TWO ? 1 : 3) * img;
@@ -595,7 +566,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
   float* L2 = (float*)(smem + (TWO ? 2 : 4) * img);
   float* Dv = L2 + npad;
   float* cs = Dv + npad;  // [NW][3*HD] bias-grad partials
-  char* dsi = (char*)(cs + NW * 3 * HD);   // SDS: [npad][npad] bf16
 
   const int HH = H * HD;
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
@@ -605,13 +575,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
                             O, dO, a.ld_o, a.lse + ((int64_t)b * H + h) * n, 1.f / (a.scale * LOG2E), n, npad);
   for (int i = threadIdx.x; i < NW * 3 * HD; i += NTH) cs[i] = 0.f;
   const int nkt = (n + 15) >> 4;
-  if (SDS) {
-    // phase 1 writes dS rows for keys < 16 nkt; phase 2 reads keys < npad:
-    // the (at most 16) rows in between are zero
-    v4u* tail = (v4u*)(dsi + (size_t)nkt * 16 * npad * 2);
-    const int nv = (npad - nkt * 16) * npad * 2 / 16;
-    for (int i = threadIdx.x; i < nv; i += NTH) tail[i] = v4u{0u, 0u, 0u, 0u};
-  }
   __syncthreads();
   ASTAMP(1);
   if (a.colsum_partial && threadIdx.x < NW * HD) {
@@ -674,14 +637,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
           P[u][i] = p;
           dS[u][i] = p * dp[i];
         }
-        if (SDS) {
-          // row key, queries q0 + 4g .. +3; padding keys stored as zeros (their
-          // exp2(-lse) may overflow and would meet K's zero rows as 0 * inf)
-          v2u pk;
-          pk[0] = kok ? pack2bf(dS[u][0], dS[u][1]) : 0u;
-          pk[1] = kok ? pack2bf(dS[u][2], dS[u][3]) : 0u;
-          *(v2u*)(dsi + dsimg_off(key, (q0 >> 2) + g, npad)) = pk;
-        }
       }
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) {
@@ -710,7 +665,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
     __syncthreads();
   }
   // ---------------- phase 2: dQ (wave owns 16-query tiles)
-  if (SDS) __syncthreads();   // every wave's dS columns are in LDS
   ASTAMP(3);
   float cq[HD / 16][4];  // per-lane running sum of this wave's dQ rows (q-bias gradient)
 #pragma unroll
@@ -724,14 +678,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
     v4f dq[HD / 16];
 #pragma unroll
     for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = v4f{0, 0, 0, 0};
-    if constexpr (SDS) {
-      for (int kc = 0; kc < npad; kc += 32) {
-        const v8s bds = ds_frag(dsi, kc, q0, lane, npad);
-#pragma unroll
-        for (int dt = 0; dt < HD / 16; ++dt)
-          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<HD>(Ki, kc, 16 * dt, lane), bds, dq[dt], 0, 0, 0);
-      }
-    } else {
     RowFrag<T, HD> qf[HD / 32], df[HD / 32];
 #pragma unroll
     for (int ks = 0; ks < HD / 32; ++ks) {
@@ -769,7 +715,6 @@ attn_bwd_kernel(const maeclip_attn_args a) {
       }
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mma_rowsum<T, HD>(Ki, kc, 16 * dt, dST[0], dST[1], dq[dt], lane);
-    }
     }
     if (qok) {
       T* rowp = dqkv + (int64_t)q * a.ld_dqkv + h * HD;
@@ -1407,34 +1352,32 @@ template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
-template <typename T, int HD, bool SDS, bool TWO = false, int OCC = 1, int WG = MAXW>
+template <typename T, int HD, bool TWO = false, int OCC = 1, int WG = MAXW>
 void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, SDS, TWO, OCC, WG>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, SDS, TWO, OCC, WG>), grid, dim3(nthreads), lds, s, a);
+    maeclip::allow_lds((const void*)attn_bwd_kernel<T, HD, TWO, OCC, WG>, (int)lds);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, TWO, OCC, WG>), grid, dim3(nthreads), lds, s, a);
 }
 
 // resident workgroups per CU of a bwd variant (registers, waves and LDS)
 template <typename T, int HD, bool TWO, int OCC = 1>
 int bwd_occupancy(int nthreads, size_t lds) {
   if (lds > 65536)
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<T, HD, false, TWO, OCC>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    maeclip::allow_lds((const void*)attn_bwd_kernel<T, HD, TWO, OCC>, (int)lds);
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)attn_bwd_kernel<T, HD, false, TWO, OCC>,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)attn_bwd_kernel<T, HD, TWO, OCC>,
                                                    nthreads, lds) != hipSuccess)
     return 0;
   return nb;
 }
 
 // bf16: use the two-image backward when it keeps more workgroups per CU
-// resident (MAECLIP_ATTN_TWO=0 / 1 forces it off / on); cached per shape.
+// resident (option ATTN_TWO = 0 / 1 / 3 forces it); cached per shape.
 // returns 0 (four images), 1 (two images) or 3 (two images, 3 workgroups / CU)
 template <int HD>
 int bwd_two(int n, int nw, size_t lds4, size_t lds2) {
-  const char* e = getenv("MAECLIP_ATTN_TWO");
-  if (e && *e) return *e == '0' ? 0 : *e == '3' && HD == 32 ? 3 : 1;
+  const int forced = maeclip::option(MAECLIP_OPT_ATTN_TWO, -1);
+  if (forced >= 0) return forced == 0 ? 0 : forced == 3 && HD == 32 ? 3 : 1;
   static int cache[2][64][MAXW + 1] = {};   // (npad / 32) x nw -> variant + 1
   const int key = ((n + 31) >> 5) & 63;
   int& c = cache[HD == 64][key][nw];
@@ -1468,8 +1411,8 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     }
   }
   if constexpr (!std::is_same<T, bf16_t>::value) {
-    // fp32 beyond the LDS images (MAECLIP_ATTN_ROWS=1 forces it: tests)
-    if (lds > 163840 || getenv_flag("MAECLIP_ATTN_ROWS")) return run_rows<HD>(a, bwd, s);
+    // fp32 beyond the LDS images (option ATTN_ROWS = 1 forces it: tests)
+    if (lds > 163840 || maeclip::option(MAECLIP_OPT_ATTN_ROWS, 0) != 0) return run_rows<HD>(a, bwd, s);
   }
   MC_CHECK_ARG(lds <= 163840, "maeclip_attn: n=%d needs %zu B of LDS (> 160 KiB)", a.n, lds);
   MC_CHECK_ARG(!bwd || !a.key_mask, "maeclip_attn_bwd: key_mask is supported by the fp32 rows path only");
@@ -1482,15 +1425,14 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     // round (profiles/r03/attn_diag64_ab.txt); with the per-wave round flags
     // it wins at the long rows only (C1 encoder n = 197: 299 -> 289 us; C2
     // encoder n = 50: 52 -> 55; C4 n = 145 even; profiles/r05/attn_diag64_ab_r5ag.txt),
-    // so it is the default for npad >= 192 (MAECLIP_ATTN_DIAG=1 / 0 forces it on / off).
-    const char* e = getenv("MAECLIP_ATTN_DIAG");
+    // so it is the default for npad >= 192 (option ATTN_DIAG = 1 / 0 forces it on / off).
+    const int od = maeclip::option(MAECLIP_OPT_ATTN_DIAG, -1);
     const int npad = (a.n + 31) & ~31;
     const size_t ld = bwd_diag_lds<HD>(a.n);
-    const bool want = HD == 32 ? !(e && *e == '0') : (e && *e ? *e == '1' : npad >= 192);
+    const bool want = HD == 32 ? od != 0 : (od >= 0 ? od == 1 : npad >= 192);
     if (bwd && npad <= 256 && ld <= 163840 && want && !a.key_mask) {
       if (ld > 65536)
-        (void)hipFuncSetAttribute((const void*)attn_bwd_diag_kernel<HD>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)ld);
+        maeclip::allow_lds((const void*)attn_bwd_diag_kernel<HD>, (int)ld);
       hipLaunchKernelGGL(attn_bwd_diag_kernel<HD>, grid, dim3(2 * npad), ld, s, a);
       MC_CHECK_LAUNCH("maeclip_attn_bwd(diag)");
       return 0;
@@ -1500,47 +1442,40 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     // bf16 rows beyond the diagonal kernel with more 16-row tiles than MAXW
     // waves: the two-image layout with up to 16 waves, default at HD 32 (C4
     // decoder n = 577: 604 -> 555 us; at HD 64 the C4 encoder, n = 145, loses:
-    // 147 -> 168; profiles/r05/attn_bw16_ab_r5ah.txt). MAECLIP_ATTN_BW16=1 / 0
+    // 147 -> 168; profiles/r05/attn_bw16_ab_r5ah.txt). Option ATTN_BW16 = 1 / 0
     // forces it on / off.
-    const char* e16 = getenv("MAECLIP_ATTN_BW16");
-    const bool bw16 = e16 && *e16 ? *e16 != '0' : HD == 32;
+    const int o16 = maeclip::option(MAECLIP_OPT_ATTN_BW16, -1);
+    const bool bw16 = o16 >= 0 ? o16 != 0 : HD == 32;
     if (bwd && tiles > MAXW && bw16) {
       const int nw16 = tiles < 16 ? tiles : 16;
       const size_t lds16 = bwd_lds<T, HD>(a.n, nw16, true);
       if (lds16 <= 163840) {
-        launch_bwd<T, HD, false, true, 1, 16>(a, grid, 64 * nw16, lds16, s);
+        launch_bwd<T, HD, true, 1, 16>(a, grid, 64 * nw16, lds16, s);
         MC_CHECK_LAUNCH("maeclip_attn_bwd(16 waves)");
         return 0;
       }
     }
   }
   if (bwd) {
-    // bf16, opt-in (MAECLIP_ATTN_SDS=1): keep dS in LDS between the two phases
-    // when the n x n image fits. Measured slower on MI355X at the path's shapes
-    // (decoder n = 197, hd = 32: 355 vs 224 us; the 100 KB image halves the
-    // workgroups per CU), so the default recomputes S / dP for dQ.
-    const size_t npad = (size_t)((a.n + 31) & ~31);
-    const size_t lds_sds = lds + npad * npad * 2;
-    bool sds = false;
+    // (round 2 also had a bf16 variant that kept dS in LDS between the two
+    // phases instead of recomputing S / dP for dQ: 355 vs 224 us at the
+    // decoder shape, the n x n image halving the workgroups per CU; removed)
     if constexpr (std::is_same<T, bf16_t>::value) {
-      sds = !two && lds_sds <= 163840 && getenv_flag("MAECLIP_ATTN_SDS");
-      if (sds) launch_bwd<T, HD, true>(a, grid, nthreads, lds_sds, s);
-      else if (variant == 3) launch_bwd<T, HD, false, true, HD == 32 ? 3 : 1>(a, grid, nthreads, lds, s);
-      else if (two) launch_bwd<T, HD, false, true>(a, grid, nthreads, lds, s);
+      if (variant == 3) launch_bwd<T, HD, true, HD == 32 ? 3 : 1>(a, grid, nthreads, lds, s);
+      else if (two) launch_bwd<T, HD, true>(a, grid, nthreads, lds, s);
     }
-    if (!sds && !two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
+    if (!two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
     auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true> : attn_fwd_kernel<T, HD, false>;
     int nth = nthreads;
     // one workgroup per CU by LDS and more tiles than MAXW waves: up to 16
-    // waves (MAECLIP_ATTN_FW16=0 turns it off)
-    const char* e16 = getenv("MAECLIP_ATTN_FW16");
-    if (tiles > MAXW && 2 * lds > 163840 && !(e16 && *e16 == '0')) {
+    // waves (option ATTN_FW16 = 0 turns it off)
+    if (tiles > MAXW && 2 * lds > 163840 && maeclip::option(MAECLIP_OPT_ATTN_FW16, 1) != 0) {
       const int r16 = (tiles + 15) / 16;
       nth = 64 * ((tiles + r16 - 1) / r16);
       kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true, 16> : attn_fwd_kernel<T, HD, false, 16>;
     }
-    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lds > 65536) maeclip::allow_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(nth), lds, s, a);
   }
   MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");

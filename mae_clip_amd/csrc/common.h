@@ -32,6 +32,12 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 // ---------------------------------------------------------------- host errors
 namespace maeclip {
 void set_error(const char* fmt, ...);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for a kernel only when a
+// launch needs more dynamic LDS than was allowed before (runtime.hip): one
+// call per kernel in practice, none per launch
+void allow_lds(const void* kernel, int bytes);
+// plan option `key` (MAECLIP_OPT_*), or dflt when unset (runtime.hip)
+int option(int key, int dflt);
 }
 
 #define MC_CHECK_ARG(cond, ...)                  \

@@ -242,7 +242,7 @@ int launch2(const maeclip_gemm_args& a, hipStream_t s) {
   const int S = a.splitk > 1 ? a.splitk : 1;
   const size_t lds = (size_t)2 * (BM + BN) * 128;
   auto kern = gemm2_kernel<BM, BN, WM, WN, LA, LB, OutT, EPI>;
-  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (lds > 65536) maeclip::allow_lds((const void*)kern, (int)lds);
   hipLaunchKernelGGL(kern, dim3(gm * gn, S, (unsigned)a.batch), dim3(WM * WN * 64), lds, s, a);
   MC_CHECK_LAUNCH("maeclip_gemm(v2)");
   return 0;

@@ -1113,10 +1113,9 @@ int gemm4_ncu() {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  // diagnostic: MAECLIP_GEMM_GRID caps the persistent grid of plain launches
+  // diagnostic: option GEMM_GRID caps the persistent grid of plain launches
   // (contention scans, tools/gemm_grid_scan.py); unset in production
-  const char* e = getenv("MAECLIP_GEMM_GRID");
-  const int cap = (e && *e) ? atoi(e) : 0;
+  const int cap = maeclip::option(MAECLIP_OPT_GEMM_GRID, 0);
   return cap > 0 && cap < ncu ? cap : ncu;
 }
 
@@ -1135,35 +1134,33 @@ struct TileChoice {
 int64_t sk_workspace_bytes(int ncu) { return SK_CNT_BYTES + 2 * (int64_t)ncu * SK_SLOT; }
 
 TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
-  const char* eb = getenv("MAECLIP_GEMM_BM");
-  const int force_bm = (eb && *eb) ? atoi(eb) : 0;
-  const char* es = getenv("MAECLIP_GEMM_SK");
+  const int force_bm = maeclip::option(MAECLIP_OPT_GEMM_BM, 0);
   // default off: in the micro-batched step every split cost whole-step
   // throughput although it wins alone (profiles/r05/gemm_split_minK_step_ab_r5i.txt)
-  const int sk_mode = (es && *es) ? atoi(es) : 0;   // 0 off, 1 cost model
-  const char* esp = getenv("MAECLIP_GEMM_SPLIT");
-  const int force_split = (esp && *esp) ? atoi(esp) : 0;
-  // the cost model's split only at K >= MAECLIP_GEMM_SPLIT_MINK (step A/B)
-  const char* emk = getenv("MAECLIP_GEMM_SPLIT_MINK");
-  const int64_t split_min_k = (emk && *emk) ? atoll(emk) : 0;
+  const int sk_mode = maeclip::option(MAECLIP_OPT_GEMM_SK, 0);   // 0 off, 1 cost model
+  const int force_split = maeclip::option(MAECLIP_OPT_GEMM_SPLIT, 0);
+  // the cost model's split only at K >= GEMM_SPLIT_MINK (step A/B)
+  const int64_t split_min_k = maeclip::option(MAECLIP_OPT_GEMM_SPLIT_MINK, 0);
   const bool plain = a.splitk <= 1 && a.batch == 1;
   const bool allow192 = force_bm != 256 && force_bm != 128 && plain && a.a_layout == LAY_KC && !a.colsum_partial;
   // 128-row tiles: bf16 only (KT 64); chosen by the cost model only when
   // MAECLIP_GEMM_BM128=1 (A/B) or forced by MAECLIP_GEMM_BM=128
-  const char* e128 = getenv("MAECLIP_GEMM_BM128");
   const bool allow128 = KT == 64 && plain && a.a_layout == LAY_KC && !a.colsum_partial &&
-                        (force_bm == 128 || (force_bm == 0 && e128 && *e128 == '1'));
+                        (force_bm == 128 || (force_bm == 0 && maeclip::option(MAECLIP_OPT_GEMM_BM128, 0) == 1));
   const bool allow256 = (force_bm != 192 || !allow192) && (force_bm != 128 || !allow128);
-  const bool allow_sk = plain && sk_mode != 0 && a.workspace != nullptr && ncu <= 256;
+  const bool allow_sk = plain && (sk_mode != 0 || force_split > 0) && a.workspace != nullptr && ncu <= 256;
   const int64_t gn = (a.N + 255) / 256, NT = a.K / KT;
   constexpr double EPI_C = 2.5, F1 = 2.0;
   const SkPlan none = {0, 0, 0, 0, nullptr, nullptr};
   // slice 0's lead per other slice (aligned split): about one publish of a
   // 256 x 256 fp32 partial; MAECLIP_GEMM_SPLIT_D overrides
-  const char* ed = getenv("MAECLIP_GEMM_SPLIT_D");
-  const int lead = (ed && *ed) ? atoi(ed) : 4;
+  const int lead = maeclip::option(MAECLIP_OPT_GEMM_SPLIT_D, 4);
   TileChoice best = {256, none};
   double best_cost = 1e30;
+  // the best data-parallel choice: the result whenever no split plan is taken
+  // (also when a forced split S does not fit the shape)
+  TileChoice best_dp = {256, none};
+  double best_dp_cost = 1e30;
   auto l0 = [&](int S) {
     // slice 0 longer by `lead` per other slice, every other slice >= 1 K-tile
     const int64_t L0 = (NT + (int64_t)(S - 1) * lead + S - 1) / S;
@@ -1184,6 +1181,10 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
     const double c = bm == 192 ? 0.89 : bm == 128 ? 0.72 : 1.0;
     const int64_t T = (a.M + bm - 1) / bm * gn, R = T % ncu;
     const double dp = (double)((T + ncu - 1) / ncu) * (NT * c + EPI_C);
+    if (dp < best_dp_cost - 1e-9) {
+      best_dp_cost = dp;
+      best_dp = {bm, none};
+    }
     if (dp < best_cost - 1e-9 && force_split == 0) {
       best_cost = dp;
       best = {bm, none};
@@ -1202,12 +1203,12 @@ TileChoice choose_tiles(const maeclip_gemm_args& a, int KT, int ncu) {
       }
     }
   }
-  return best;
+  return best.sk.on() ? best : best_dp;
 }
 
 template <typename KernT, typename ArgT>
 void launch_persistent(KernT kern, int lds, int64_t tiles, int ncu, bool sk, const ArgT& g, hipStream_t s) {
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  maeclip::allow_lds((const void*)kern, lds);
   // one block per CU: persistent over tiles (stream-K: the whole grid, the
   // block positions the plan was made for)
   const int grid = sk ? ncu : (int)(tiles < ncu ? tiles : ncu);
@@ -1243,7 +1244,7 @@ int launch4(const maeclip_gemm_args& a, hipStream_t s) {
   }
   const int gm = (int)((a.M + 255) / 256);
   auto kern = S > 1 ? gemm4_kernel<LA, LB, OutT, EPI, true> : gemm4_kernel<LA, LB, OutT, EPI, false>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+  maeclip::allow_lds((const void*)kern, TileM<256>::LDS_ALL);
   // one block per CU (128 KiB LDS): persistent over tiles for plain launches;
   // split-K / batched launches get one block per (tile, slice, batch)
   const int tiles = gm * gn;
@@ -1356,7 +1357,7 @@ int launch_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipS
     }
   }
   auto kern = gemm4_f8_kernel<OutT, EPI, F8>;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+  maeclip::allow_lds((const void*)kern, TileM<256>::LDS_ALL);
   const int tiles = (int)(((a.M + 255) / 256) * gn);
   const int grid = (a.batch > 1 || tiles < ncu) ? tiles : ncu;
   hipLaunchKernelGGL(kern, dim3(grid, 1, (unsigned)a.batch), dim3(512), TileM<256>::LDS_ALL, s, g);
@@ -1469,8 +1470,7 @@ int wg_splits(int T, int64_t M) {
 // block's range cuts at most two tiles (two 256 KB fp32 slots). Below 8
 // K-tiles per block the slot write + reduce outweighs the balance.
 int wg_skw(int T, int64_t M) {
-  const char* e = getenv("MAECLIP_WG_SK");   // 0: uniform split-K slices instead (A/B)
-  const bool enabled = !(e && *e == '0');
+  const bool enabled = maeclip::option(MAECLIP_OPT_WG_SK, 1) != 0;   // 0: uniform split-K slices instead (A/B)
   const int G = wg_ncu(), R = T % G;
   if (R == 0 || !enabled) return 0;
   const int64_t skw = ((int64_t)R * (M / 64) + G - 1) / G;
@@ -1563,7 +1563,7 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       g.S = 1;
       g.NT = (int)(M / 64);
       g.Tdp = T - T % wg_ncu();
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      maeclip::allow_lds((const void*)wgrad4_kernel<false>, TileM<256>::LDS_ALL);
       hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(wg_ncu()), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(stream-k)");
       hipLaunchKernelGGL(wgrad4_sk_reduce_kernel, dim3(T - g.Tdp, SKR_CHUNKS), dim3(256), 0, s, g);
@@ -1580,7 +1580,7 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
     }
     const int units = T * g.S, grid = std::min(units, wg_ncu());
     if (g.S > 1) {
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      maeclip::allow_lds((const void*)wgrad4_kernel<true>, TileM<256>::LDS_ALL);
       hipLaunchKernelGGL(wgrad4_kernel<true>, dim3(grid), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
       int64_t maxnk = 0;
@@ -1589,7 +1589,7 @@ extern "C" int32_t maeclip_wgrad_grouped(const maeclip_wgrad_problem* probs, int
       hipLaunchKernelGGL(wgrad4_reduce_kernel, dim3(gx, n), dim3(256), 0, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped(reduce)");
     } else {
-      (void)hipFuncSetAttribute((const void*)wgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, TileM<256>::LDS_ALL);
+      maeclip::allow_lds((const void*)wgrad4_kernel<false>, TileM<256>::LDS_ALL);
       hipLaunchKernelGGL(wgrad4_kernel<false>, dim3(grid), dim3(512), TileM<256>::LDS_ALL, s, g);
       MC_CHECK_LAUNCH("maeclip_wgrad_grouped");
     }

@@ -67,29 +67,41 @@ def alias_stream(capture_stream, replay_stream):
         _STREAM_ALIAS[capture_stream] = replay_stream
 
 
-class gemm_split_scope:
-    """Launches issued inside the scope may take maeclip_gemm's split plan
-    (MAECLIP_GEMM_SK=1, read per launch by the library); restores the previous
-    setting on exit. Host-thread scoped: the library reads the environment."""
+def set_option(name: str, value) -> int:
+    """Set one plan option of the library (include/maeclip.h maeclip_set_option;
+    None / -1 = the built-in default); returns the previous value (-1: default).
+    The library snapshots the MAECLIP_<name> environment once; later changes of
+    the environment are not seen, this is the way to switch a plan at run time."""
+    key = L.OPTIONS.index(name)
+    return int(L.lib().maeclip_set_option(key, -1 if value is None else int(value)))
 
-    def __init__(self, enabled=True):
-        self.enabled, self.prev = enabled, None
+
+def get_option(name: str) -> int:
+    return int(L.lib().maeclip_get_option(L.OPTIONS.index(name)))
+
+
+class options:
+    """Scope of plan options: `with K.options(GEMM_BM=192, GEMM_SPLIT=2): ...`
+    sets them for the launches issued inside and restores the previous values."""
+
+    def __init__(self, **kw):
+        self.kw, self.prev = kw, {}
 
     def __enter__(self):
-        if self.enabled:
-            import os
-            self.prev = os.environ.get("MAECLIP_GEMM_SK")
-            os.environ["MAECLIP_GEMM_SK"] = "1"
+        for k, v in self.kw.items():
+            self.prev[k] = set_option(k, v)
         return self
 
     def __exit__(self, *exc):
-        if self.enabled:
-            import os
-            if self.prev is None:
-                os.environ.pop("MAECLIP_GEMM_SK", None)
-            else:
-                os.environ["MAECLIP_GEMM_SK"] = self.prev
+        for k, v in self.prev.items():
+            set_option(k, v)
         return False
+
+
+def gemm_split_scope(enabled=True):
+    """Launches issued inside the scope may take maeclip_gemm's split plan
+    (option GEMM_SK = 1); restores the previous setting on exit."""
+    return options(GEMM_SK=1) if enabled else options()
 
 
 def _stream_scratch(device, nbytes):
@@ -103,6 +115,12 @@ def _stream_scratch(device, nbytes):
     key = (device.index, _STREAM_ALIAS.get(s, s))
     t = _SCRATCH.get(key)
     if t is None or t.numel() * 4 < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            # a buffer made here would come from the graph's private pool with
+            # its zero-fill baked into every replay: the eager steps before a
+            # capture (graph.CapturedStep) size the replay stream's scratch
+            raise L.MaeClipNativeError(
+                f"GEMM scratch of {nbytes} B first requested inside a graph capture; run the step eagerly first")
         if t is not None:
             _SCRATCH_RETIRED.append(t)
         t = torch.zeros((nbytes + 3) // 4, device=device, dtype=torch.float32)

@@ -29,3 +29,21 @@ def dev():
     from mae_clip_amd import _lib
     _lib.load()
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def opts():
+    """set library plan options for one test (include/maeclip.h
+    maeclip_set_option; the library reads the environment only once):
+    opts(GEMM_BM=192, ...); every option set is restored afterwards"""
+    from mae_clip_amd import kernels as K
+    prev = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            old = K.set_option(k, v)
+            prev.setdefault(k, old)
+
+    yield set_
+    for k, v in prev.items():
+        K.set_option(k, v)

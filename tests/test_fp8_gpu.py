@@ -83,15 +83,15 @@ def _deq(op):
 @pytest.mark.parametrize("bm", ["auto", "192", "sk", "sk192"])
 @pytest.mark.parametrize("afmt", [K.FP8_E4M3, K.FP8_E5M2])
 @pytest.mark.parametrize("mnk", [(512, 384, 256), (1000, 768, 1024), (2308, 512, 2048), (9280, 1024, 512)])
-def test_gemm_fp8_vs_dequantised_fp64(dev, afmt, mnk, bm, monkeypatch):
+def test_gemm_fp8_vs_dequantised_fp64(dev, afmt, mnk, bm, opts):
     """C = (s_A q_A)(s_B q_B)^T: the operands are exact in fp64, so the only
     error is the fp32 accumulation (and the bf16 / fp32 output rounding).
     bm = "192": the 192-row tile variant forced (N = 1024 at M = 9280 picks it
     by itself, like the C4 encoder's N = 1024 shapes)."""
     if bm in ("192", "sk192"):
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+        opts(GEMM_BM=192)
     if bm.startswith("sk"):   # stream-K forced wherever the tiles leave a partial last round
-        monkeypatch.setenv("MAECLIP_GEMM_SK", "1")
+        opts(GEMM_SK=1)
     M, N, Kd = mnk
     g = torch.Generator().manual_seed(M + N)
     x = (torch.randn(M, Kd, generator=g) * 3).to(torch.bfloat16).to(dev)

@@ -42,10 +42,10 @@ def test_gemm_layouts(dev, dtype, lay, mnk):
 @pytest.mark.parametrize("mnk", [(12800, 768, 768), (1000, 520, 192), (50000, 512, 256), (192, 256, 64), (193, 264, 128),
                                  (12800, 3072, 768), (6400, 768, 3072), (300, 264, 64)])
 @pytest.mark.parametrize("bm", ["192", "128"])
-def test_gemm_bm192(dev, b_lay, mnk, bm, monkeypatch):
+def test_gemm_bm192(dev, b_lay, mnk, bm, opts):
     """192- and 128-row tiles of the v4 kernel (forced): ragged M / N, one tile, several persistent tiles per
     block (M = 50000: 261 x 2 tiles on 256 CUs at 192 rows), one K-tile, KC x KC and KC x RC."""
-    monkeypatch.setenv("MAECLIP_GEMM_BM", bm)
+    opts(GEMM_BM=int(bm))
     M, N, Kd = mnk
     A = _rand((M, Kd), torch.bfloat16, dev, seed=1)
     B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, seed=2)
@@ -56,6 +56,20 @@ def test_gemm_bm192(dev, b_lay, mnk, bm, monkeypatch):
         err = (C.double() - ref).abs().max().item()
         scale = ref.abs().max().item() + 1e-6
         assert err / scale < (2e-5 * math.sqrt(Kd) if out == torch.float32 else 1e-2), (out, err, scale)
+
+
+def _ncu(dev):
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def _plan_workspace(dev, M, N, Kd, b_lay):
+    """scratch bytes maeclip_gemm asks for this plain bf16 launch under the
+    current options (> 0: a split plan was chosen)"""
+    import ctypes
+    from mae_clip_amd import _lib as L
+    a = L.GemmArgs(A=16, B=16, C=16, M=M, N=N, K=Kd, lda=Kd, ldb=Kd if b_lay == 0 else N, ldc=N, batch=1,
+                   dtype=L.BF16, out_dtype=L.F32, a_layout=0, b_layout=b_lay, alpha=1.0, splitk=1)
+    return int(L.lib().maeclip_gemm_workspace(ctypes.byref(a)))
 
 
 def _sk_counters_zero():
@@ -70,7 +84,7 @@ def _sk_counters_zero():
 @pytest.mark.parametrize("mnk", [(6400, 768, 3072), (6400, 2304, 768), (25216, 512, 2048), (50432, 512, 1536),
                                  (1000, 520, 192), (300, 264, 640), (12800, 768, 768)])
 @pytest.mark.parametrize("mode", ["auto", "split2_192", "split2_192_lead0", "split2_192_lead9"])
-def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
+def test_gemm_stream_k(dev, b_lay, mnk, mode, opts):
     """Split plain launches (every tile's K range cut into S slices, the
     slices summed in the same launch by the block that arrives last, gemm4.hip
     sk_fixup): forced on 192-row tiles ("split2_192", slice 0's lead per
@@ -82,13 +96,20 @@ def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
     vs fp64; bitwise equal on repeat (the summation order is fixed whichever
     block arrives last); counters left zero."""
     if mode.startswith("split"):
-        monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+        opts(GEMM_SPLIT=int(mode[5]))
+        opts(GEMM_BM=192)
     else:
-        monkeypatch.setenv("MAECLIP_GEMM_SK", "1")   # the cost model (off by default)
+        opts(GEMM_SK=1)   # the cost model (off by default)
     if "_lead" in mode:
-        monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
+        opts(GEMM_SPLIT_D=int(mode.split("_lead")[1]))
     M, N, Kd = mnk
+    if mode.startswith("split"):
+        # the forced split is taken wherever it fits (tiles <= 256, 2 slices
+        # per tile <= 2 rounds of the grid, >= 2 K-tiles per slice), else the
+        # best data-parallel plan: the workspace query says which
+        T = -(-M // 192) * -(-N // 256)
+        fits = T <= 256 and 2 * T <= 2 * _ncu(dev) and Kd // 64 >= 4
+        assert (_plan_workspace(dev, M, N, Kd, b_lay) > 0) == fits, (mnk, T)
     A = _rand((M, Kd), torch.bfloat16, dev, seed=11)
     B = _rand((N, Kd) if b_lay == 0 else (Kd, N), torch.bfloat16, dev, scale=0.5, seed=12)
     ref = _ref_mm(A, B.t() if b_lay == 0 else B)
@@ -106,19 +127,21 @@ def test_gemm_stream_k(dev, b_lay, mnk, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["split2_192", "split2_192_lead0", "bm128"])
-def test_gemm_stream_k_epilogues(dev, mode, monkeypatch):
+def test_gemm_stream_k_epilogues(dev, mode, opts):
     """Every fused epilogue behind the split fix-up (the last block runs it
     on the summed tile): bias + GELU / GELU' (aux_out), fp32 residual, column
     sums, dGELU, mul-aux + residual; M = 3000 x N = 768 (36 / 48 tiles, every
     tile cut) at K = 1024."""
     if mode == "bm128":   # the 128-row tile's epilogues (no split)
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "128")
+        opts(GEMM_BM=128)
     else:
-        monkeypatch.setenv("MAECLIP_GEMM_SPLIT", mode[5])
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+        opts(GEMM_SPLIT=int(mode[5]))
+        opts(GEMM_BM=192)
     if "_lead" in mode:
-        monkeypatch.setenv("MAECLIP_GEMM_SPLIT_D", mode.split("_lead")[1])
+        opts(GEMM_SPLIT_D=int(mode.split("_lead")[1]))
     M, N, Kd = 3000, 768, 1024
+    if mode != "bm128":   # 16 x 3 tiles: every tile is cut
+        assert _plan_workspace(dev, M, N, Kd, 0) > 0
     x = _rand((M, Kd), torch.bfloat16, dev, seed=13)
     w = _rand((N, Kd), torch.bfloat16, dev, scale=0.03, seed=14)
     bias = _rand((N,), torch.float32, dev, seed=15)
@@ -157,13 +180,13 @@ def test_gemm_stream_k_epilogues(dev, mode, monkeypatch):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M", [300, 700])   # fp32: 32x32-tile small kernel / 128x128 MFMA kernel
 @pytest.mark.parametrize("bm", ["auto", "192"])
-def test_gemm_epilogues(dev, dtype, M, bm, monkeypatch):
+def test_gemm_epilogues(dev, dtype, M, bm, opts):
     """bm = "192": every epilogue on 192-row tiles (forced; colsum launches keep
     256)."""
     if bm != "auto":
         if dtype == torch.float32:
             pytest.skip("192-row tiles: bf16 operands")
-        monkeypatch.setenv("MAECLIP_GEMM_BM", "192")
+        opts(GEMM_BM=192)
     N, Kd = 384, 256
     x = _rand((M, Kd), dtype, dev, seed=3)
     w = _rand((N, Kd), dtype, dev, scale=0.05, seed=4)
@@ -218,19 +241,18 @@ def _attn_ref(qkv, B, n, H, hd, scale, key_mask=None):
     return (p @ v).transpose(1, 2).reshape(B * n, H * hd)
 
 
-@pytest.mark.parametrize("mode", ["four", "two", "two3", "sds", "diag", "bw16", "rows"])
+@pytest.mark.parametrize("mode", ["four", "two", "two3", "diag", "bw16", "rows"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 50, 3, 64), (2, 197, 2, 64), (2, 37, 4, 32), (3, 5, 2, 32), (1, 130, 2, 64),
                                    (1, 197, 2, 32), (1, 256, 2, 64), (2, 224, 2, 32), (1, 577, 2, 32),
                                    (2, 145, 2, 64), (2, 256, 2, 32)])
-def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
+def test_attention_fwd_bwd(dev, dtype, shape, mode, opts):
     """fp32 parity mode holds two [n][hd] f32 images at a time in the
     backward, so the C1 encoder (n = 197, hd = 64) runs in fp32 as well. bf16
     backward variants: four LDS images ("four"), two images with K/V (phase 1)
     and Q/dO (phase 2) tiles from HBM ("two", picked when it fits more
     workgroups per CU; "two3": its 3-workgroups-per-CU register budget at
-    hd = 32), dS kept in LDS between the phases ("sds", opt-in), one-pass
-    diagonal schedule with dQ accumulated in LDS ("diag": bf16, n <= 256 at
+    hd = 32), one-pass diagonal schedule with dQ accumulated in LDS ("diag": bf16, n <= 256 at
     hd = 32, n <= 224 at hd = 64; the default there). fp32 beyond its LDS images (n = 577, the C4
     decoder) streams 64-row blocks through LDS ("rows"; forced here at every
     shape, picked by itself at n = 577 in "four"); "bw16": the two-image
@@ -241,17 +263,14 @@ def test_attention_fwd_bwd(dev, dtype, shape, mode, monkeypatch):
         pytest.skip("fp32 parity mode: MFMA kernel (two images) or the rows path")
     if dtype == torch.bfloat16 and mode == "rows":
         pytest.skip("rows path: fp32 parity mode only")
-    monkeypatch.setenv("MAECLIP_ATTN_ROWS", "1" if mode == "rows" else "0")
+    opts(ATTN_ROWS=1 if mode == "rows" else 0)
     if mode == "diag" and (dtype == torch.float32 or n > (256 if hd == 32 else 224)):
         pytest.skip("diagonal backward: bf16, n <= 256 at hd 32, n <= 224 at hd 64")
-    monkeypatch.setenv("MAECLIP_ATTN_DIAG", "1" if mode == "diag" else "0")
+    opts(ATTN_DIAG=1 if mode == "diag" else 0)
     if mode == "bw16" and (dtype == torch.float32 or n <= 128):
         pytest.skip("16-wave backward: bf16 with more than 8 16-row tiles")
-    monkeypatch.setenv("MAECLIP_ATTN_BW16", "1" if mode == "bw16" else "0")
-    monkeypatch.setenv("MAECLIP_ATTN_TWO", {"two": "1", "two3": "3"}.get(mode, "0"))
-    if mode == "sds":
-        # bf16 backward keeps dS in LDS for dQ instead of recomputing S/dP (opt-in)
-        monkeypatch.setenv("MAECLIP_ATTN_SDS", "1")
+    opts(ATTN_BW16=1 if mode == "bw16" else 0)
+    opts(ATTN_TWO={"two": 1, "two3": 3}.get(mode, 0))
     scale = hd ** -0.5
     qkv = _rand((B * n, 3 * H * hd), dtype, dev, seed=11)
     o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
@@ -290,10 +309,10 @@ def test_attention_key_mask(dev):
 
 
 @pytest.mark.parametrize("rows", [False, True])
-def test_attention_key_mask_f32(dev, rows, monkeypatch):
+def test_attention_key_mask_f32(dev, rows, opts):
     """fp32 parity mode with DistilBERT's key-padding mask, MFMA kernel and the
     long-sequence rows path; the backward of the rows path honours the mask too."""
-    monkeypatch.setenv("MAECLIP_ATTN_ROWS", "1" if rows else "0")
+    opts(ATTN_ROWS=1 if rows else 0)
     B, n, H, hd = 3, 70, 2, 64
     qkv = _rand((B * n, 3 * H * hd), torch.float32, dev, seed=14)
     km = torch.ones((B, n), device=dev)
@@ -518,7 +537,7 @@ def test_wgrad_splitk_v4(dev, mnk):
 
 @pytest.mark.parametrize("case", ["encoder4", "decoder2x4", "few_tiles_splitk", "strided", "fp32_fallback",
                                   "whole_plus_streamk", "uniform_slices"])
-def test_wgrad_grouped(dev, case, monkeypatch):
+def test_wgrad_grouped(dev, case, opts):
     """maeclip_wgrad_grouped: the 4 weight gradients of transformer blocks
     (qkv, proj, fc1, fc2) in one launch vs fp64 torch; stream-K remainder
     (fewer tiles than CUs; whole tiles + a remainder dealt out by K-tiles, with
@@ -532,7 +551,7 @@ def test_wgrad_grouped(dev, case, monkeypatch):
     elif case in ("decoder2x4", "uniform_slices"):
         M, shapes = 6400, [(1536, 512), (512, 512), (2048, 512), (512, 2048)] * 2
         if case == "uniform_slices":
-            monkeypatch.setenv("MAECLIP_WG_SK", "0")
+            opts(WG_SK=0)
     elif case == "whole_plus_streamk":
         # 144 + 108 + 132 = 384 tiles: 256 whole, 128 (2600-row edge tiles among
         # them) over the grid by K-tiles
@@ -747,9 +766,17 @@ def test_image_preprocess_resize_bit_exact(dev):
     assert np.array_equal(out, ref)
 
 
-@pytest.mark.parametrize("shape", [(64, 50, 12, 64), (8, 197, 16, 32), (4, 197, 12, 64), (16, 25, 12, 64)])
+@pytest.mark.parametrize("shape", [(64, 50, 12, 64), (8, 197, 16, 32), (4, 197, 12, 64), (16, 25, 12, 64),
+                                   # production grids of the kernels that order their waves with
+                                   # per-wave LDS flags (many co-resident workgroups per CU):
+                                   (256, 197, 16, 32),    # C2 decoder: diagonal backward, 4096 workgroups
+                                   (128, 197, 16, 32),    # C2 decoder micro-batch
+                                   (256, 197, 12, 64),    # C1 encoder: hd-64 diagonal backward at n = 197
+                                   (128, 577, 16, 32)])   # C4 decoder: 16-wave forward and backward
 def test_attention_deterministic(dev, shape):
-    """fwd and bwd are bitwise reproducible (no atomics; fixed reduction order)."""
+    """fwd and bwd are bitwise reproducible (no atomics; fixed reduction order),
+    also at the full production grids where the diagonal backward's waves
+    drift apart by up to a round between their flag waits."""
     B, n, H, hd = shape
     qkv = _rand((B * n, 3 * H * hd), torch.bfloat16, dev, seed=31)
     dout = _rand((B * n, H * hd), torch.bfloat16, dev, seed=32)
