@@ -129,6 +129,31 @@ template <bool E5> __device__ __forceinline__ unsigned mc_cvt4_fp8(float a, floa
   return (unsigned)r;
 }
 
+// fp8 BLOCKS (MX-style operands of v_mfma_scale_f32_16x16x128_f8f6f4; maeclip.h
+// "fp8 blocks"): one e8m0 exponent per 32 consecutive K-elements of a row.
+// The exponent is the smallest power of two 2^(e-127) with amax / 2^(e-127) <=
+// FMT_MAX (448 = 1.75 * 2^8 for e4m3, 57344 = 1.75 * 2^15 for e5m2), taken from
+// the bits of amax: no division, and x * 2^(127-e) is exact, so q =
+// rne(x * 2^(127-e)) never overflows. amax = 0 gives e = 0 (q = 0).
+__device__ __forceinline__ unsigned mc_e8m0(float amax, bool e5) {
+  const unsigned u = __float_as_uint(amax);
+  int e = (int)(u >> 23) - (e5 ? 15 : 8) + ((u & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return (unsigned)(e < 0 ? 0 : e);
+}
+// 2^(127 - e): the quantisation multiplier of exponent e (e <= 253)
+__device__ __forceinline__ float mc_e8m0_inv(unsigned e) { return __uint_as_float((254u - e) << 23); }
+// byte offset of the scale of row r, K-block b (32 elements) in a scale tensor
+// for K = 128 T: [row / 64][K-tile b / 4][block b % 4][row % 16][(row / 16) % 4].
+// The GEMM reads, per K-tile, one 256-byte run per 64-row group: lane (row
+// fragment r % 16, block g) the dword holding the scales of rows r, r + 16,
+// r + 32, r + 48, selected by the MFMA's scale byte select.
+__host__ __device__ __forceinline__ int64_t mc_fp8b_off(int64_t r, int64_t b, int64_t T) {
+  return ((((r >> 6) * T + (b >> 2)) << 8) | ((b & 3) << 6) | ((r & 15) << 2) | ((r >> 4) & 3));
+}
+__host__ __device__ __forceinline__ int64_t mc_fp8b_bytes(int64_t rows, int64_t K) {
+  return (rows + 63) / 64 * 64 * (K / 32);
+}
+
 // erf-GELU (nn.GELU() / HF "gelu" / timm default) and its derivative sharing
 // one exp: Phi(x) = 0.5 erfc(-x/sqrt2) with erfc by Abramowitz & Stegun 7.1.26
 // (|err| <= 1.5e-7; |gelu err| <= 4.2e-7 over [-12,12], the same as f32 erff),

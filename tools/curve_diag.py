@@ -8,6 +8,7 @@ compares the losses with the fp64 curve the reference itself produced
   A  product (fp32 parity mode) + HIP AdamW          (the test)
   B  product (fp32 parity mode) + torch.optim.AdamW  (same forward / backward, torch's update on the GPU)
   D  oracle fp32 on the CPU + torch.optim.AdamW
+  F  oracle fp32 on the GPU (torch's own kernels) + torch.optim.AdamW
   E  oracle fp64 on the CPU + torch.optim.AdamW       (must reproduce the golden curve)
 
 and prints, per step, |dloss| / loss vs the golden curve, plus the step-0
@@ -40,13 +41,17 @@ def build(kind, dev):
         m = CLIPModel()
     if kind == "product":
         return m.to(dev).eval()
+    if kind == "fp32gpu":
+        ref = RefCLIP(oracle_config(**kw))
+        ref.load_state_dict({k: v.detach().clone() for k, v in m.state_dict().items()}, strict=True)
+        return ref.float().to(dev).eval()
     ref = RefCLIP(oracle_config(**kw))
     ref.load_state_dict({k: v.detach().clone() for k, v in m.state_dict().items()}, strict=True)
     return (ref.double() if kind == "fp64" else ref.float()).eval()
 
 
 def run(kind, opt_kind, dev, steps, grads0=None):
-    m = build("product" if kind == "product" else kind, dev)
+    m = build(kind, dev)
     params = [p for p in m.parameters() if p.requires_grad]
     if opt_kind == "hip":
         from mae_clip_amd.optim import AdamW
@@ -56,7 +61,7 @@ def run(kind, opt_kind, dev, steps, grads0=None):
     losses, g0 = [], None
     for k in range(steps):
         b = make_batch(8, 32, seed=300 + k)
-        if kind == "product":
+        if kind in ("product", "fp32gpu"):
             b = {kk: v.to(dev) for kk, v in b.items()}
         else:
             b = dict(b, image=b["image"].to(torch.float64 if kind == "fp64" else torch.float32))
@@ -80,7 +85,8 @@ def main():
     gold = [float(x) for x in z["losses"]][:a.steps]
     res = {}
     for name, kind, optk in [("A_product_hipadamw", "product", "hip"), ("B_product_torchadamw", "product", "torch"),
-                             ("D_oracle_fp32", "fp32", "torch"), ("E_oracle_fp64", "fp64", "torch")]:
+                             ("D_oracle_fp32", "fp32", "torch"), ("F_oracle_fp32_gpu_torch", "fp32gpu", "torch"),
+                             ("E_oracle_fp64", "fp64", "torch")]:
         losses, g0 = run(kind, optk, dev, a.steps)
         rel = [abs(l - g) / abs(g) for l, g in zip(losses, gold)]
         res[name] = {"losses": losses, "rel": rel, "worst": max(rel), "worst_step": int(np.argmax(rel)), "g0": g0}
