@@ -124,6 +124,15 @@ typedef struct {
   float* colsum_partial;
   int32_t splitk;
   float* workspace;
+  /* optional fp8-blocks copy of the output (bf16 C only, N % 128 == 0): q8
+   * [M, ldq8] bytes of format q8_fmt and e8m0 block scales q8_scale
+   * (maeclip_fp8b_scale_bytes(M, N) bytes), the quantisation of the bf16 C as
+   * stored (bit-identical to maeclip_quant_blocks_fp8 of C): the next fp8
+   * GEMM's A operand without a separate pass */
+  void* q8;
+  int64_t ldq8;
+  uint8_t* q8_scale;
+  int32_t q8_fmt;
 } maeclip_gemm_args;
 int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
 /* fp8 GEMM (C4 path; replaces the nn.Linear matmuls of the timm / ViTMAE
@@ -134,6 +143,25 @@ int32_t maeclip_gemm(const maeclip_gemm_args* args, void* stream);
  * scale_a[m] * scale_b[n] * alpha before bias / epilogue (args->epilogue as
  * maeclip_gemm; no split-K, beta must be 0). M, N >= 256, N % 8 == 0. */
 int32_t maeclip_gemm_fp8(const maeclip_gemm_args* args, const float* scale_a, const float* scale_b, void* stream);
+/* fp8 BLOCKS (the MX layout of the block-scaled MFMA): a row of K elements is
+ * cut into K / 32 blocks, each quantised with its own power-of-two scale
+ * 2^(e - 127), e an e8m0 byte: e = the smallest exponent with amax(block) /
+ * 2^(e - 127) <= FMT_MAX, q = rne(x * 2^(127 - e)); x ~= q * 2^(e - 127). A
+ * producer that owns only part of a row (a GEMM epilogue tile, an attention
+ * head) can quantise it without the whole-row amax a per-row scale needs.
+ * Scale bytes are laid out for the GEMM's reads (K % 128 == 0):
+ *   byte (r, b) at (((r / 64) * (K / 128) + b / 4) * 256 + (b % 4) * 64 +
+ *                   (r % 16) * 4 + (r / 16) % 4)
+ * maeclip_fp8b_scale_bytes(rows, K) = ceil(rows / 64) * 64 * K / 32. */
+int64_t maeclip_fp8b_scale_bytes(int64_t rows, int64_t K);
+/* x (bf16 / f32 [rows, ld]) -> fp8 blocks q [rows, ldq] + scales (cols % 128 == 0) */
+int32_t maeclip_quant_blocks_fp8(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ld, void* q,
+                                 int64_t ldq, uint8_t* scales, int32_t fmt, void* stream);
+/* fp8 GEMM with an fp8-blocks A operand: as maeclip_gemm_fp8, the A block
+ * scales (e8m0, the layout above, K = args->K) applied by the MFMA itself,
+ * B (e4m3) scaled per column by scale_b in the epilogue. */
+int32_t maeclip_gemm_fp8_blocks(const maeclip_gemm_args* args, const uint8_t* scale_a, const float* scale_b,
+                                void* stream);
 /* Row-wise fp8 quantisation: q[r, :] = rne(x[r, :] / s[r]), s[r] = amax(x[r, :]) /
  * FMT_MAX (1 when the row is zero). x bf16 or f32 [rows, ld]; q [rows, ldq]
  * bytes; fmt MAECLIP_FP8_E4M3 (activations, weights) or _E5M2 (gradients). */

@@ -30,7 +30,8 @@ class GemmArgs(C.Structure):
                 ("epilogue", c_i32), ("alpha", c_f32), ("beta", c_f32),
                 ("bias", c_vp), ("aux", c_vp), ("aux_out", c_vp), ("ldaux", c_i64),
                 ("resid", c_vp), ("ldr", c_i64), ("colsum_partial", c_vp),
-                ("splitk", c_i32), ("workspace", c_vp)]
+                ("splitk", c_i32), ("workspace", c_vp),
+                ("q8", c_vp), ("ldq8", c_i64), ("q8_scale", c_vp), ("q8_fmt", c_i32)]
 
 
 class AttnArgs(C.Structure):
@@ -154,6 +155,9 @@ _SIGS = {
     "maeclip_gemm_splitk": (c_i32, [c_i64, c_i64, c_i64]),
     "maeclip_gemm_fp8": (c_i32, [C.POINTER(GemmArgs), c_vp, c_vp, c_vp]),
     "maeclip_quant_rows_fp8": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "maeclip_fp8b_scale_bytes": (c_i64, [c_i64, c_i64]),
+    "maeclip_quant_blocks_fp8": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp]),
+    "maeclip_gemm_fp8_blocks": (c_i32, [C.POINTER(GemmArgs), c_vp, c_vp, c_vp]),
     "maeclip_quant_cols_fp8_workspace": (c_i64, [c_i64, c_i64]),
     "maeclip_quant_weights_fp8_prepare": (c_i64, [C.POINTER(Fp8wEntry), c_i32]),
     "maeclip_quant_weights_fp8": (c_i32, [c_vp, C.POINTER(Fp8wEntry), c_i32, c_vp, c_i64, c_vp]),

@@ -64,6 +64,8 @@ text_attention_dropout = 0.1
 
 # ---- numerics / determinism
 precision = "bf16"         # "bf16" (perf), "fp8" (C4: e4m3/e5m2 stack GEMMs, bf16 elsewhere) or "fp32" (parity mode)
+fp8_grad_format = "e4m3"   # fp8 mode: the dgrad GEMMs' gradient operand, "e4m3" (3 mantissa bits; the block / row
+                           # scales give it the range) or "e5m2" (2 mantissa bits, wider range)
 mask_seed = 2
 dropout_seed = 1234
 # ---- scheduling

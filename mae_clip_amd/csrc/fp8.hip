@@ -292,7 +292,75 @@ __global__ void __launch_bounds__(256) wq_cols_kernel(const maeclip_fp8w_entry* 
   }
 }
 
+// fp8 blocks (maeclip_quant_blocks_fp8): one wave per row, 8 consecutive
+// elements per lane and 512-column chunk, so a 32-element block is the 4 lanes
+// of a DPP quad: its amax is two quad-permute max steps, its e8m0 exponent
+// mc_e8m0, written by the quad's first lane at mc_fp8b_off.
+template <typename T, bool E5>
+__global__ void __launch_bounds__(256) quant_blocks_kernel(const T* __restrict__ x, int64_t rows, int cols, int64_t ld,
+                                                           uint8_t* __restrict__ q, int64_t ldq,
+                                                           uint8_t* __restrict__ sc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int KT = cols / 128;
+  const T* xr = x + row * ld;
+  uint8_t* qr = q + row * ldq;
+  for (int c0 = 0; c0 < cols; c0 += 512) {
+    const int e = c0 + lane * 8;
+    float w[8];
+    float amax = 0.f;
+    if (e < cols) {
+      Row8<T>::load(xr + e, w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(w[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = 0.f;
+    }
+    amax = fmaxf(amax, dpp_mov<0xB1>(amax));   // quad_perm [1,0,3,2]
+    amax = fmaxf(amax, dpp_mov<0x4E>(amax));   // quad_perm [2,3,0,1]
+    const unsigned ex = mc_e8m0(amax, E5);
+    const float inv = mc_e8m0_inv(ex);
+    if (e < cols) {
+      v2u o;
+      o[0] = cvt4<E5>(w[0] * inv, w[1] * inv, w[2] * inv, w[3] * inv);
+      o[1] = cvt4<E5>(w[4] * inv, w[5] * inv, w[6] * inv, w[7] * inv);
+      *(v2u*)(qr + e) = o;
+      if ((lane & 3) == 0) sc[mc_fp8b_off(row, e >> 5, KT)] = (uint8_t)ex;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int64_t maeclip_fp8b_scale_bytes(int64_t rows, int64_t K) {
+  return rows > 0 && K > 0 && K % 128 == 0 ? mc_fp8b_bytes(rows, K) : 0;
+}
+
+extern "C" int32_t maeclip_quant_blocks_fp8(const void* x, int32_t x_dtype, int64_t rows, int64_t cols, int64_t ld,
+                                            void* q, int64_t ldq, uint8_t* scales, int32_t fmt, void* stream) {
+  MC_CHECK_ARG(x && q && scales && rows >= 0 && cols > 0, "maeclip_quant_blocks_fp8: bad arguments");
+  MC_CHECK_ARG(x_dtype == MAECLIP_BF16 || x_dtype == MAECLIP_F32, "maeclip_quant_blocks_fp8: x dtype bf16 or f32");
+  MC_CHECK_ARG(fmt == MAECLIP_FP8_E4M3 || fmt == MAECLIP_FP8_E5M2, "maeclip_quant_blocks_fp8: bad fp8 format");
+  MC_CHECK_ARG(cols % 128 == 0 && ld % 8 == 0 && ldq % 8 == 0 && ld >= cols && ldq >= cols,
+               "maeclip_quant_blocks_fp8: cols %% 128, ld and ldq %% 8");
+  MC_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 7) == 0, "maeclip_quant_blocks_fp8: alignment");
+  MC_CHECK_ARG(cols < (1 << 30), "maeclip_quant_blocks_fp8: row too long");
+  if (rows == 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  const bool e5 = fmt == MAECLIP_FP8_E5M2;
+  if (x_dtype == MAECLIP_BF16) {
+    if (e5) hipLaunchKernelGGL((quant_blocks_kernel<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t*)x, rows, (int)cols, ld, (uint8_t*)q, ldq, scales);
+    else hipLaunchKernelGGL((quant_blocks_kernel<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)x, rows, (int)cols, ld, (uint8_t*)q, ldq, scales);
+  } else {
+    if (e5) hipLaunchKernelGGL((quant_blocks_kernel<float, true>), grid, dim3(256), 0, s, (const float*)x, rows, (int)cols, ld, (uint8_t*)q, ldq, scales);
+    else hipLaunchKernelGGL((quant_blocks_kernel<float, false>), grid, dim3(256), 0, s, (const float*)x, rows, (int)cols, ld, (uint8_t*)q, ldq, scales);
+  }
+  MC_CHECK_LAUNCH("maeclip_quant_blocks_fp8");
+  return 0;
+}
 
 // host side of the batched weight quantisation: prefix sums filled here
 extern "C" int64_t maeclip_quant_weights_fp8_prepare(maeclip_fp8w_entry* host, int32_t n) {

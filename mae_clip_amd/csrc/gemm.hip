@@ -32,6 +32,7 @@ namespace maeclip {
 int gemm_v2(const maeclip_gemm_args& a, hipStream_t s, int variant);
 int gemm_v4(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_v4_ok(const maeclip_gemm_args& a);
+int check_q8(const maeclip_gemm_args& a, const char* who);
 int64_t gemm_v4_workspace(const maeclip_gemm_args& a);
 int gemm_small(const maeclip_gemm_args& a, hipStream_t s);
 bool gemm_small_ok(const maeclip_gemm_args& a);
@@ -420,6 +421,7 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
                  "maeclip_gemm: split-K needs a workspace, epilogue 0 and no colsum");
     MC_CHECK_ARG(a->ldc == a->N, "maeclip_gemm: split-K output must be dense (ldc == N)");
   }
+  if (int e = maeclip::check_q8(*a, "maeclip_gemm")) return e;
   hipStream_t s = (hipStream_t)stream;
   // v2 (LDS-DMA, larger tiles) for every bf16 shape with 64-aligned K
   static const int forced = getenv("MAECLIP_GEMM_VARIANT") ? atoi(getenv("MAECLIP_GEMM_VARIANT")) : 0;
@@ -431,7 +433,17 @@ extern "C" int32_t maeclip_gemm(const maeclip_gemm_args* a, void* stream) {
   // split tiles with an in-launch fix-up when the tiles leave most of the grid
   // idle) wherever its shape conditions hold; MAECLIP_GEMM_VARIANT=1..7 pins a
   // v2 tile, 99 v1
-  if ((forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a))
+  const bool v4 = (forced == 0 || forced == 8) && maeclip::gemm_v4_ok(*a);
+  // every path but v4 (whose epilogue writes it): the fp8-blocks copy of C
+  // (q8) by a second pass
+  if (a->q8 && !v4) {
+    maeclip_gemm_args b = *a;
+    b.q8 = nullptr;
+    if (int e = maeclip_gemm(&b, stream)) return e;
+    return maeclip_quant_blocks_fp8(a->C, MAECLIP_BF16, a->M, a->N, a->ldc, a->q8, a->ldq8, a->q8_scale, a->q8_fmt,
+                                    stream);
+  }
+  if (v4)
     rc = maeclip::gemm_v4(*a, s);
   else if (a->dtype == MAECLIP_BF16 && forced != 99 && a->K % 64 == 0 && a->K > 0 && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
            (a->a_layout == LAY_KC || a->M >= 8) && (a->b_layout == LAY_KC || a->N >= 8))

@@ -30,6 +30,10 @@
 #include <stdlib.h>
 #include "../../include/maeclip.h"
 
+namespace maeclip {
+int check_q8(const maeclip_gemm_args& a, const char* who);
+}
+
 namespace {
 
 enum { LAY_KC = 0, LAY_RC = 1 };
@@ -60,7 +64,11 @@ template <int BM> struct TileM {
   static constexpr int HALF_A = BM / 2 * 128;        // bytes per A half image
   static constexpr int BUF_T = 2 * HALF_A + 2 * HALF;
   static constexpr int LDS_T = 2 * BUF_T;                      // operand stages
-  static constexpr int LDS_ALL = LDS_T + 8 * 4096;               // + epilogue scratch (8 waves x 4 KiB)
+  // BM = 192: fp8-blocks A scales, one 1 KiB image per K-tile stage (the 3
+  // 64-row groups of the tile + a dummy slot, 256 B each)
+  static constexpr int SC_T = BM == 192 ? 2048 : 0;
+  static constexpr int SCR_OFF = LDS_T + SC_T;
+  static constexpr int LDS_ALL = SCR_OFF + 8 * 4096;             // + epilogue scratch (8 waves x 4 KiB)
   __device__ static __forceinline__ int hoff(int h) { return h < 2 ? h * HALF_A : 2 * HALF_A + (h - 2) * HALF; }
 };
 
@@ -194,10 +202,41 @@ __device__ __forceinline__ void pin_quad(v4f (&acc)[2 * MI][4], int i0, int j0) 
 #endif
 }
 
+// F8 = 3 / 4 (fp8-blocks A, e4m3 / e5m2): the A fragment i of the half takes
+// its e8m0 block scale from byte i of `sc` (the MFMA's scale byte select), B's
+// scale is 2^0 (its per-column scale is applied in the epilogue). Measured
+// operand layout of the 16x16x128 form (tools/mfma_scale_probe.py,
+// profiles/r06/mfma_scale_probe.json): lane group g holds K [16 g, 16 g + 16)
+// in its first four VGPRs and K [64 + 16 g, ...) in the last four -- the two
+// 16-B chunks g and 4 + g of the K-tile row that frag() reads -- and the scale
+// of lane l applies to row l % 16 and K-block l / 16 = K [32 (l / 16), +32):
+// a K-block's 32 elements sit in two lane groups, its scale in a third lane's
+// VGPR, which is what the scale tensor's layout hands each lane.
+template <int AF, int I>
+__device__ __forceinline__ v4f mfma_blk(v8i b, v8i a, v4f c, unsigned sc) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, 0, AF, 0, 127, I, (int)sc);
+}
 template <int F8, int MI>
 __device__ __forceinline__ void quad_mma(v4f (&acc)[2 * MI][4], int i0, int j0, const v8s (&fbq)[2][2],
-                                         const v8s (&fa)[MI][2]) {
-  if constexpr (F8 == 0) {
+                                         const v8s (&fa)[MI][2], unsigned sc = 0) {
+  if constexpr (F8 >= 3) {
+    constexpr int AF = F8 == 4 ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const v8i a8 = cat_frag(fa[i][0], fa[i][1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const v8i b8 = cat_frag(fbq[j][0], fbq[j][1]);
+        v4f& c = acc[i0 + i][j0 + j];
+        switch (i) {
+          case 0: c = mfma_blk<AF, 0>(b8, a8, c, sc); break;
+          case 1: c = mfma_blk<AF, 1>(b8, a8, c, sc); break;
+          case 2: c = mfma_blk<AF, 2>(b8, a8, c, sc); break;
+          default: c = mfma_blk<AF, 3>(b8, a8, c, sc); break;
+        }
+      }
+    }
+  } else if constexpr (F8 == 0) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -420,7 +459,7 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
 #pragma unroll
         for (int r = 0; r < 4; ++r) x[4 * v + r] = t[r];
       }
-      const float rsc = F8 ? sa[min(m, M - 1)] : 1.f;
+      const float rsc = (F8 && sa) ? sa[min(m, M - 1)] : 1.f;   // fp8-blocks A: scaled in the MFMA
 #pragma unroll
       for (int v = 0; v < VPL; ++v) x[v] = F8 ? fmaf(x[v] * rsc, csc[v], bias[v]) : fmaf(x[v], alpha, bias[v]);
       const bool ok = m < M && nok;
@@ -471,6 +510,35 @@ __device__ __forceinline__ void epilogue4(const maeclip_gemm_args& args, v4f (&a
       if (LOAD_RES && has_res) {
 #pragma unroll
         for (int v = 0; v < VPL; ++v) x[v] += rs[c % PF][q][v / 4][v % 4];
+      }
+      if (L8 && args.q8) {
+        // fp8-blocks copy of the bf16 row segment as stored (maeclip.h q8):
+        // a 32-column block is the lane quad 4k .. 4k + 3 (8 columns each)
+        float xs[VPL], am = 0.f;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          xs[v] = bf2f(f2bf(x[v]));
+          am = fmaxf(am, fabsf(xs[v]));
+        }
+        am = fmaxf(am, dpp_mov<0xB1>(am));
+        am = fmaxf(am, dpp_mov<0x4E>(am));
+        const bool e5 = args.q8_fmt == MAECLIP_FP8_E5M2;
+        const unsigned ex = mc_e8m0(am, e5);
+        const float inv = mc_e8m0_inv(ex);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) xs[v] *= inv;
+        if (ok) {
+          v2u o;
+          if (e5) {
+            o[0] = mc_cvt4_fp8<true>(xs[0], xs[1], xs[2], xs[3]);
+            o[1] = mc_cvt4_fp8<true>(xs[4 % VPL], xs[5 % VPL], xs[6 % VPL], xs[7 % VPL]);
+          } else {
+            o[0] = mc_cvt4_fp8<false>(xs[0], xs[1], xs[2], xs[3]);
+            o[1] = mc_cvt4_fp8<false>(xs[4 % VPL], xs[5 % VPL], xs[6 % VPL], xs[7 % VPL]);
+          }
+          NT_ST(o, (v2u*)((uint8_t*)args.q8 + (int64_t)m * args.ldq8 + n));
+          if ((lane & 3) == 0) args.q8_scale[mc_fp8b_off(m, n >> 5, N >> 7)] = (uint8_t)ex;
+        }
       }
       if (ok) {
         OutT* cp = C + (int64_t)m * args.ldc + n;
@@ -567,6 +635,7 @@ struct Gemm4Args {
   SkPlan sk;
   const float* sa;    // fp8 only: per-row A / per-column B dequantisation scales
   const float* sb;
+  const uint8_t* sab; // fp8-blocks A: e8m0 block scales (common.h mc_fp8b_off layout)
 };
 
 // Fix-up of one split tile (slice u.slot of S = 2): returns true in the block
@@ -676,8 +745,16 @@ struct WgGroup {
 template <int LA, int LB, typename OutT, int EPI, bool SPLIT, bool GRP, int F8 = 0, int BM = 256, bool SK = false>
 __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const WgGroup* __restrict__ gp,
                                            const float* __restrict__ sa = nullptr,
-                                           const float* __restrict__ sb = nullptr, const SkPlan* skp_ = nullptr) {
+                                           const float* __restrict__ sb = nullptr, const SkPlan* skp_ = nullptr,
+                                           const uint8_t* __restrict__ sab = nullptr) {
   static_assert(F8 == 0 || (LA == LAY_KC && LB == LAY_KC && !SPLIT && !GRP), "fp8: KC x KC plain launches only");
+  // fp8-blocks A (F8 3 / 4): 192-row tiles, no split plan. The three 64-row
+  // scale groups of a K-tile ride with its Bn1 half: waves 4-6 issue one
+  // 256-B LDS-DMA each (wave 7 a dummy copy), so every wave keeps 6 DMA
+  // instructions in the three youngest halves (waves 0-3: 2 + 2 + 2, waves
+  // 4-7: 1 + 2 + 3) and one counted wait serves all.
+  constexpr bool F8B = F8 >= 3;
+  static_assert(!F8B || (BM == 192 && !SK), "fp8-blocks A: 192-row tiles without a split plan");
   static_assert(BM == 256 || ((BM == 192 || BM == 128) && LA == LAY_KC && !SPLIT && !GRP),
                 "BM 192 / 128: KC A, plain launches only");
   static_assert(!SK || (!SPLIT && !GRP), "stream-K: plain launches only");
@@ -689,7 +766,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  char* const scr = smem + TM::LDS_T + wave * EPI_SCR;   // this wave's epilogue scratch
+  char* const scr = smem + TM::SCR_OFF + wave * EPI_SCR;   // this wave's epilogue scratch
   const int64_t z = GRP ? 0 : blockIdx.z;
 
   // units: standard = output tiles (this block's slice is blockIdx.y);
@@ -844,6 +921,15 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       const rsrc_t rs = LB == LAY_KC ? make_rsrc(w.B + (int64_t)w.n0 * w.ldb * ESZ, ((int64_t)w.N - w.n0) * w.ldb * ESZ)
                                      : make_rsrc(w.B + (int64_t)w.n0 * ESZ, ((int64_t)w.K * w.ldb - w.n0) * ESZ);
       issue_half(rs, vB[h - 2][0], vB[h - 2][1], k0 * (LB == LAY_KC ? ESZ : (int)(w.ldb * ESZ)), dst, wave);
+      if constexpr (F8B) {
+        if (h == 3 && wave >= 4) {
+          const int T8 = w.K / KT;
+          const int G = w.m0 / 64 + min(wave - 4, 2);
+          const rsrc_t rsc = make_rsrc((const char*)sab, mc_fp8b_bytes(w.M, w.K));
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (lds_void*)(smem + TM::LDS_T + (t & 1) * 1024 + (wave - 4) * 256),
+                                                   4, lane * 4, (G * T8 + w.kbeg / KT + t) * 256, 0, 0);
+        }
+      }
     }
   };
   // K-tile 0 whole + three halves of K-tile 1 (its Am1 follows in p0)
@@ -866,7 +952,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
   // 2 + 2 + 2 wave-instructions, or 1 + 2 + 2 for waves 4-7 at BM 192 and
   // every wave at BM 128
   auto wait_halves = [&]() {
-    if (BM == 256 || (BM == 192 && wave < 4)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (BM == 256 || (BM == 192 && (wave < 4 || F8B))) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   };
 #ifdef GEMM4_STAMPS
@@ -897,7 +983,21 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       // GELU epilogues with aux_out also store a bf16 pre-activation / GELU'
       // per chunk: twice the bf16 stores, all younger than this tile's DMA
       const bool two_out = (EPI == EPI_GELU || EPI == EPI_GELU_D) && args.aux_out != nullptr && !GRP;
-      if (BM == 256) {
+      // an fp8-blocks copy (q8) adds two stores per bf16 store instruction
+      // (the fp8 bytes, the quad's scale byte)
+      const bool q8 = sizeof(OutT) == 2 && args.q8 != nullptr && !GRP;
+      if (q8) {
+        if (BM == 256) {
+          if (two_out) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+        } else if (BM == 128) {
+          if (two_out) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        } else {
+          if (two_out) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        }
+      } else if (BM == 256) {
         if (sizeof(OutT) == 2 && two_out) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
         else if (sizeof(OutT) == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
@@ -928,8 +1028,20 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
     v8s fa[MI][2], fb[2][2][2];
+    // fp8-blocks: the A scale dword of half `sub` for this lane (row lane % 16,
+    // block lane / 16): the 16-row groups 6 wm + 3 sub .. +2 of the tile, byte i
+    // = fragment i after the byte align
+    auto read_sc = [&](const char* img, int sub) -> unsigned {
+      const int g16 = 6 * wm + 3 * sub;
+      const int o = (lane >> 4) * 64 + (lane & 15) * 4;
+      const unsigned lo = *(const unsigned*)(img + (g16 >> 2) * 256 + o);
+      const unsigned hi = *(const unsigned*)(img + ((g16 + 2) >> 2) * 256 + o);
+      return __builtin_amdgcn_alignbyte(hi, lo, (unsigned)(g16 & 3));
+    };
+    unsigned sc0 = 0, sc1 = 0;
     for (int t = 0; t < nt; ++t) {
       const char* buf = smem + (t & 1) * TM::BUF_T;
+      const char* scimg = smem + TM::LDS_T + (t & 1) * 1024;
       const char* hA0 = buf;
       const char* hA1 = buf + TM::HALF_A;
       const char* hB0 = buf + 2 * TM::HALF_A;
@@ -944,11 +1056,12 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA0, (BM / 4) * wm + 16 * i, ks, lane);
+      if constexpr (F8B) sc0 = read_sc(scimg, 0);
       if (more1) issue(u, voA, voB, t + 1, 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8, MI>(acc, 0, 0, fb[0], fa);
+      quad_mma<F8, MI>(acc, 0, 0, fb[0], fa, sc0);
       if constexpr (!GRP || (GEMM4_PIN_GRP >> 0) & 1) pin_quad<MI>(acc, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
@@ -961,7 +1074,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       LGKM_EARLY();
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8, MI>(acc, 0, 2, fb[1], fa);
+      quad_mma<F8, MI>(acc, 0, 2, fb[1], fa, sc0);
       if constexpr (!GRP || (GEMM4_PIN_GRP >> 1) & 1) pin_quad<MI>(acc, 0, 2);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
@@ -970,11 +1083,12 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(hA1, (BM / 4) * wm + 16 * i, ks, lane);
+      if constexpr (F8B) sc1 = read_sc(scimg, 1);
       if (more2) issue(u, voA, voB, t + 2, 2);
       LGKM_EARLY();
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8, MI>(acc, MI, 2, fb[1], fa);
+      quad_mma<F8, MI>(acc, MI, 2, fb[1], fa, sc1);
       if constexpr (!GRP || (GEMM4_PIN_GRP >> 2) & 1) pin_quad<MI>(acc, MI, 2);
       __builtin_amdgcn_s_setprio(0);
       SEG_BARRIER();
@@ -996,7 +1110,7 @@ __device__ __forceinline__ void gemm4_body(const maeclip_gemm_args& args, const 
       }
       SEG_BARRIER();
       __builtin_amdgcn_s_setprio(1);
-      quad_mma<F8, MI>(acc, MI, 0, fb[0], fa);
+      quad_mma<F8, MI>(acc, MI, 0, fb[0], fa, sc1);
       if constexpr (!GRP || (GEMM4_PIN_GRP >> 3) & 1) pin_quad<MI>(acc, MI, 0);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 || more1) SEG_BARRIER();   // group 1 skips its very last one (it took one extra up front)
@@ -1050,7 +1164,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const Gemm4Args g) {
 // fp8 operands (maeclip_gemm_fp8): KC x KC, per-row / per-column scales
 template <typename OutT, int EPI, int F8, int BM = 256, bool SK = false>
 __global__ void __launch_bounds__(512) gemm4_f8_kernel(const Gemm4Args g) {
-  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8, BM, SK>(g.a, nullptr, g.sa, g.sb, &g.sk);
+  gemm4_body<LAY_KC, LAY_KC, OutT, EPI, false, false, F8, BM, SK>(g.a, nullptr, g.sa, g.sb, &g.sk, g.sab);
 }
 
 // grouped weight gradients: RC x RC, fp32 out, no epilogue (beta only)
@@ -1381,32 +1495,88 @@ int epi_f8(const maeclip_gemm_args& a, const float* sa, const float* sb, hipStre
 #endif
 }
 
+// fp8-blocks A (maeclip_gemm_fp8_blocks): 192-row tiles (the scale images fit
+// beside their operand stages there), no split plan
+template <typename OutT, int EPI, int F8>
+int launch_f8b(const maeclip_gemm_args& a, const uint8_t* sab, const float* sb, hipStream_t s) {
+  const int ncu = gemm4_ncu();
+  Gemm4Args g = {};
+  g.a = a;
+  g.sb = sb;
+  g.sab = sab;
+  const int64_t tiles = (a.M + 191) / 192 * ((a.N + 255) / 256);
+  launch_persistent(gemm4_f8_kernel<OutT, EPI, F8, 192>, TileM<192>::LDS_ALL, tiles, ncu, false, g, s);
+  MC_CHECK_LAUNCH("maeclip_gemm_fp8_blocks");
+  return 0;
+}
+
+template <typename OutT, int F8>
+int epi_f8b(const maeclip_gemm_args& a, const uint8_t* sab, const float* sb, hipStream_t s) {
+  switch (a.epilogue) {
+    case EPI_NONE: return launch_f8b<OutT, EPI_NONE, F8>(a, sab, sb, s);
+    case EPI_RESID: return launch_f8b<OutT, EPI_RESID, F8>(a, sab, sb, s);
+    case EPI_GELU_D: return launch_f8b<OutT, EPI_GELU_D, F8>(a, sab, sb, s);
+    case EPI_MUL_AUX: return launch_f8b<OutT, EPI_MUL_AUX, F8>(a, sab, sb, s);
+    default: MC_CHECK_ARG(false, "maeclip_gemm_fp8_blocks: epilogue %d not built (0, 2, 4, 5)", a.epilogue);
+  }
+}
+
+// argument checks shared by the two fp8 entries
+int check_f8(const maeclip_gemm_args* a, const char* who) {
+  MC_CHECK_ARG(a->dtype == MAECLIP_FP8_E4M3 || a->dtype == MAECLIP_FP8_E5M2,
+               "%s: dtype (A format) must be MAECLIP_FP8_E4M3 or MAECLIP_FP8_E5M2", who);
+  MC_CHECK_ARG(a->a_layout == LAY_KC && a->b_layout == LAY_KC, "%s: KC x KC operands only", who);
+  MC_CHECK_ARG(a->K > 0 && a->K % 128 == 0, "%s: K=%lld must be a positive multiple of 128", who, (long long)a->K);
+  MC_CHECK_ARG(a->M >= 256 && a->N >= 256 && a->N % 8 == 0, "%s: M, N >= 256 and N %% 8 == 0", who);
+  MC_CHECK_ARG(a->splitk <= 1, "%s: no split-K", who);
+  MC_CHECK_ARG(a->batch >= 1, "%s: batch >= 1", who);
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  MC_CHECK_ARG(al16(a->A) && al16(a->B) && a->lda % 16 == 0 && a->ldb % 16 == 0 && a->lda >= a->K && a->ldb >= a->K,
+               "%s: operands need 16-B aligned rows (lda, ldb %% 16 == 0, >= K)", who);
+  MC_CHECK_ARG(al16(a->C) && (a->out_dtype == MAECLIP_BF16 ? a->ldc % 8 : a->ldc % 4) == 0, "%s: C alignment", who);
+  const bool wa = a->epilogue == EPI_GELU || a->epilogue == EPI_GELU_D;
+  const bool ra = a->epilogue == EPI_DGELU || a->epilogue == EPI_MUL_AUX;
+  MC_CHECK_ARG(!(wa && a->aux_out && (!al16(a->aux_out) || a->ldaux % 8)) && !(ra && (!al16(a->aux) || a->ldaux % 8)),
+               "%s: aux alignment", who);
+  MC_CHECK_ARG(!a->resid || (al16(a->resid) && a->ldr % 4 == 0), "%s: resid alignment", who);
+  MC_CHECK_ARG(!a->bias || al16(a->bias), "%s: bias alignment", who);
+  const int64_t lim = 0x7fffffffLL;
+  MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "%s: operand exceeds 2^31 bytes", who);
+  return maeclip::check_q8(*a, who);
+}
+
 }  // namespace
+
+namespace maeclip {
+// the optional fp8-blocks output of a GEMM (maeclip_gemm_args q8)
+int check_q8(const maeclip_gemm_args& a, const char* who) {
+  if (!a.q8) return 0;
+  MC_CHECK_ARG(a.out_dtype == MAECLIP_BF16 && a.batch == 1 && a.beta == 0.f && a.splitk <= 1 && a.N % 128 == 0 &&
+                   a.ldq8 >= a.N && a.ldq8 % 8 == 0 && ((uintptr_t)a.q8 & 7) == 0 && a.q8_scale &&
+                   (a.q8_fmt == MAECLIP_FP8_E4M3 || a.q8_fmt == MAECLIP_FP8_E5M2),
+               "%s: fp8-blocks output (q8) needs bf16 C, batch 1, beta 0, N %% 128 == 0, ldq8 %% 8, a scale buffer "
+               "and an fp8 format", who);
+  return 0;
+}
+}  // namespace maeclip
+
+extern "C" int32_t maeclip_gemm_fp8_blocks(const maeclip_gemm_args* a, const uint8_t* scale_a, const float* scale_b,
+                                           void* stream) {
+  MC_CHECK_ARG(a != nullptr && scale_a != nullptr && scale_b != nullptr, "maeclip_gemm_fp8_blocks: null argument");
+  if (int e = check_f8(a, "maeclip_gemm_fp8_blocks")) return e;
+  MC_CHECK_ARG(a->batch == 1 && ((uintptr_t)scale_b & 15) == 0, "maeclip_gemm_fp8_blocks: batch 1, 16-B aligned scale_b");
+  hipStream_t s = (hipStream_t)stream;
+  const bool e5 = a->dtype == MAECLIP_FP8_E5M2;
+  if (a->out_dtype == MAECLIP_BF16)
+    return e5 ? epi_f8b<bf16_t, 4>(*a, scale_a, scale_b, s) : epi_f8b<bf16_t, 3>(*a, scale_a, scale_b, s);
+  return e5 ? epi_f8b<float, 4>(*a, scale_a, scale_b, s) : epi_f8b<float, 3>(*a, scale_a, scale_b, s);
+}
 
 extern "C" int32_t maeclip_gemm_fp8(const maeclip_gemm_args* a, const float* scale_a, const float* scale_b,
                                     void* stream) {
   MC_CHECK_ARG(a != nullptr && scale_a != nullptr && scale_b != nullptr, "maeclip_gemm_fp8: null argument");
-  MC_CHECK_ARG(a->dtype == MAECLIP_FP8_E4M3 || a->dtype == MAECLIP_FP8_E5M2,
-               "maeclip_gemm_fp8: dtype (A format) must be MAECLIP_FP8_E4M3 or MAECLIP_FP8_E5M2");
-  MC_CHECK_ARG(a->a_layout == LAY_KC && a->b_layout == LAY_KC, "maeclip_gemm_fp8: KC x KC operands only");
-  MC_CHECK_ARG(a->K > 0 && a->K % 128 == 0, "maeclip_gemm_fp8: K=%lld must be a positive multiple of 128",
-               (long long)a->K);
-  MC_CHECK_ARG(a->M >= 256 && a->N >= 256 && a->N % 8 == 0, "maeclip_gemm_fp8: M, N >= 256 and N %% 8 == 0");
-  MC_CHECK_ARG(a->splitk <= 1, "maeclip_gemm_fp8: no split-K");
-  MC_CHECK_ARG(a->batch >= 1, "maeclip_gemm_fp8: batch >= 1");
-  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  MC_CHECK_ARG(al16(a->A) && al16(a->B) && a->lda % 16 == 0 && a->ldb % 16 == 0 && a->lda >= a->K && a->ldb >= a->K,
-               "maeclip_gemm_fp8: operands need 16-B aligned rows (lda, ldb %% 16 == 0, >= K)");
-  MC_CHECK_ARG(al16(a->C) && (a->out_dtype == MAECLIP_BF16 ? a->ldc % 8 : a->ldc % 4) == 0 && al16(scale_b),
-               "maeclip_gemm_fp8: C / scale_b alignment");
-  const bool wa = a->epilogue == EPI_GELU || a->epilogue == EPI_GELU_D;
-  const bool ra = a->epilogue == EPI_DGELU || a->epilogue == EPI_MUL_AUX;
-  MC_CHECK_ARG(!(wa && a->aux_out && (!al16(a->aux_out) || a->ldaux % 8)) && !(ra && (!al16(a->aux) || a->ldaux % 8)),
-               "maeclip_gemm_fp8: aux alignment");
-  MC_CHECK_ARG(!a->resid || (al16(a->resid) && a->ldr % 4 == 0), "maeclip_gemm_fp8: resid alignment");
-  MC_CHECK_ARG(!a->bias || al16(a->bias), "maeclip_gemm_fp8: bias alignment");
-  const int64_t lim = 0x7fffffffLL;
-  MC_CHECK_ARG(a->M * a->lda < lim && a->N * a->ldb < lim, "maeclip_gemm_fp8: operand exceeds 2^31 bytes");
+  if (int e = check_f8(a, "maeclip_gemm_fp8")) return e;
+  MC_CHECK_ARG(((uintptr_t)scale_b & 15) == 0, "maeclip_gemm_fp8: 16-B aligned scale_b");
   hipStream_t s = (hipStream_t)stream;
   const bool e5 = a->dtype == MAECLIP_FP8_E5M2;
   if (a->out_dtype == MAECLIP_BF16)

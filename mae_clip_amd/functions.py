@@ -145,24 +145,44 @@ class StackSpec:
     w8: list = None                 # fp8 mode: per block ((W, W^T) fp8 operands) x (qkv, proj, fc1, fc2)
 
 
-def _fwd(x, w, w8, xq=None, **kw):
-    """Forward GEMM of a stack: bf16 / fp32 (w), or fp8 (w8 = (W, W^T)): x is
-    quantised per token (e4m3; xq: already quantised by its producer, the
-    LayerNorm) and multiplied with W (per output channel)."""
+def _quant8(x, fmt, colsum):
+    """fp8 operand of x made by a separate pass (its producer wrote none):
+    fp8 blocks, or per-row scales for a launch with column sums (those run on
+    the 256-row tile, which has no room for the block scales' LDS images)"""
+    return K.quant_rows_fp8(x, fmt) if colsum is not None else K.quant_blocks_fp8(x, fmt)
+
+
+def _fwd(x, w, w8, xq=None, q8=None, **kw):
+    """Forward GEMM of a stack: bf16 / fp32 (w), or fp8 (w8 = (W, W^T)): x in
+    e4m3 (xq: already quantised by its producer -- per token by a LayerNorm,
+    fp8 blocks by a GEMM epilogue; else a pass here) times W (per output
+    channel); q8: an Fp8Blocks the epilogue fills with the output's fp8 copy."""
     if w8 is None:
-        return K.linear_fwd(x, w, **kw)
+        return K.linear_fwd(x, w, q8=q8, **kw)
     kw.setdefault("out_dtype", x.dtype)
-    return K.linear_fp8(xq if xq is not None else K.quant_rows_fp8(x, K.FP8_E4M3), w8[0], **kw)
+    xq = xq if xq is not None else _quant8(x, K.FP8_E4M3, kw.get("colsum"))
+    return K.linear_fp8(xq, w8[0], q8=q8, **kw)
 
 
-def _dgrad(dy, w, w8, dyq=None, **kw):
-    """dgrad GEMM dX = dY W: fp8 mode quantises dY per token (e5m2, the wider
-    range of gradients; dyq: already quantised by the LayerNorm backward) and
-    multiplies with W^T (per input channel)."""
+def _gfmt():
+    """fp8 format of the gradient operands (config.fp8_grad_format)"""
+    from . import config as CFG
+    return K.FP8_E5M2 if getattr(CFG, "fp8_grad_format", "e4m3") == "e5m2" else K.FP8_E4M3
+
+
+def _dgrad(dy, w, w8, dyq=None, q8=None, **kw):
+    """dgrad GEMM dX = dY W: fp8 mode takes dY in config.fp8_grad_format
+    (dyq: already quantised by its producer) times W^T (per input channel)."""
     if w8 is None:
-        return K.linear_dgrad(dy, w, **kw)
+        return K.linear_dgrad(dy, w, q8=q8, **kw)
     kw.setdefault("out_dtype", dy.dtype)
-    return K.linear_fp8(dyq if dyq is not None else K.quant_rows_fp8(dy, K.FP8_E5M2), w8[1], **kw)
+    dyq = dyq if dyq is not None else _quant8(dy, _gfmt(), kw.get("colsum"))
+    return K.linear_fp8(dyq, w8[1], q8=q8, **kw)
+
+
+def _b8(f8, M, D, fmt, dev):
+    """Fp8Blocks for a GEMM epilogue to fill when its consumer GEMM runs in fp8."""
+    return K.new_fp8_blocks(M, D, fmt, dev) if f8 is not None else None
 
 
 def _q8(f8, M, D, fmt, dev):
@@ -294,10 +314,13 @@ class TransformerStackFn(torch.autograd.Function):
             q2 = _q8(f8[2], M, D, K.FP8_E4M3, dev)
             h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T, q8=q2)
             # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
+            # (+ a's fp8 blocks for fc2 in fp8 mode)
             dgelu = torch.empty((M, w1.shape[0]), device=dev, dtype=T)
-            a = _fwd(h2, w1, f8[2], xq=q2, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
+            a8 = _b8(f8[3], M, w1.shape[0], K.FP8_E4M3, dev)
+            a = _fwd(h2, w1, f8[2], xq=q2, q8=a8, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu)
             del q2
-            x2 = _fwd(a, w2, f8[3], bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
+            x2 = _fwd(a, w2, f8[3], xq=a8, bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1)
+            del a8
             saved.append([xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a])
             xi = x2
         ctx.saved = saved
@@ -396,17 +419,19 @@ class TransformerStackFn(torch.autograd.Function):
             # mlp.fc2 (+ GELU backward fused into the dgrad epilogue: dA = (dy W2) * gelu'(h))
             gi[11] = rb.add(cpart, out=gout(ar, p[11]))
             dA_part = torch.empty((K.gemm_colsum_rows(M), w1.shape[0]), device=g.device, dtype=torch.float32)
-            dA = _dgrad(gT, w2, f8[3], dyq=gq, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
+            dA8 = _b8(f8[2], M, w1.shape[0], _gfmt(), g.device)   # fc1's dgrad operand (fp8 mode)
+            dA = _dgrad(gT, w2, f8[3], dyq=gq, q8=dA8, epilogue=K.EPI_MUL_AUX, aux=dgelu, colsum=dA_part)
             gq = None
             gi[10] = wq.wgrad(gT, a, out=gout(ar, p[10]))
             del a, dgelu
             # mlp.fc1
             gi[9] = rb.add(dA_part, out=gout(ar, p[9]))
-            dh2 = _dgrad(dA, w1, f8[2])
+            dh2 = _dgrad(dA, w1, f8[2], dyq=dA8)
+            del dA8
             gi[8] = wq.wgrad(dA, h2, out=gout(ar, p[8]))
             del dA
             # norm2 (+ residual gradient)
-            q1 = _q8(f8[1], M, D, K.FP8_E5M2, g.device) if bf else None
+            q1 = _q8(f8[1], M, D, _gfmt(), g.device) if bf else None
             dx1, dx1T, pg, pb, pc = K.ln_bwd(dh2, x1, m2, r2, n2w, dres=g, want_bf16=bf, want_colsum=True, q8=q1)
             gi[6], gi[7] = rb.add(pg, out=gout(ar, p[6])), rb.add(pb, out=gout(ar, p[7]))
             if not bf:
@@ -426,7 +451,7 @@ class TransformerStackFn(torch.autograd.Function):
             # norm1 (+ residual gradient)
             # the next (lower) block's fc2 dgrad reads dxT: quantised here when it is fp8
             f8n = (spec.w8[i - 1][3] if spec.w8 is not None and i > 0 else None)
-            gq = _q8(f8n, M, D, K.FP8_E5M2, g.device) if bf else None
+            gq = _q8(f8n, M, D, _gfmt(), g.device) if bf else None
             dx, dxT, pg, pb, pc = K.ln_bwd(dh1, xi, m1, r1, n1w, dres=dx1, want_bf16=bf, want_colsum=True, q8=gq)
             gi[0], gi[1] = rb.add(pg, out=gout(ar, p[0])), rb.add(pb, out=gout(ar, p[1]))
             ctx.saved[i] = None

@@ -130,7 +130,7 @@ def _stream_scratch(device, nbytes):
 
 def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=EPI_NONE, alpha=1.0, beta=0.0,
          bias=None, aux=None, aux_out=None, ldaux=0, resid=None, ldr=0, colsum=None, batch=1,
-         strides=(0, 0, 0), splitk=1, workspace=None):
+         strides=(0, 0, 0), splitk=1, workspace=None, q8=None):
     _dev(A, B, Cout, bias, aux, aux_out, resid, colsum, workspace)
     if A.dtype != B.dtype:
         raise TypeError("gemm: A and B dtypes differ")
@@ -140,6 +140,7 @@ def gemm(A, B, Cout, M, N, K, lda, ldb, ldc, a_layout=KC, b_layout=KC, epilogue=
                    alpha=alpha, beta=beta, bias=_ptr(bias), aux=_ptr(aux), aux_out=_ptr(aux_out), ldaux=ldaux,
                    resid=_ptr(resid), ldr=ldr, colsum_partial=_ptr(colsum), splitk=splitk,
                    workspace=_ptr(workspace))
+    _set_q8(a, q8)
     if workspace is None and splitk <= 1:
         nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
         if nb > 0:
@@ -179,6 +180,52 @@ class Fp8Rows:
     @property
     def shape(self):
         return self.q.shape
+
+
+class Fp8Blocks:
+    """An fp8-blocks GEMM operand (include/maeclip.h "fp8 blocks", the MX
+    layout of the block-scaled MFMA): q uint8 [rows, cols] (OCP bytes) + e8m0
+    exponents e uint8, one per 32 consecutive columns of a row, in the GEMM's
+    read layout (x ~= 2^(e - 127) q). Producers that own only part of a row
+    (a GEMM epilogue tile, an attention head) write it without a whole-row
+    amax; the block-scaled MFMA applies the scales itself."""
+    __slots__ = ("q", "e", "fmt")
+
+    def __init__(self, q, e, fmt):
+        self.q, self.e, self.fmt = q, e, fmt
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+
+def fp8b_scale_bytes(rows: int, cols: int) -> int:
+    return int(L.lib().maeclip_fp8b_scale_bytes(rows, cols))
+
+
+def new_fp8_blocks(rows, cols, fmt, device):
+    """An empty Fp8Blocks for a producer to fill (a GEMM's q8 output, ...)."""
+    return Fp8Blocks(torch.empty((rows, cols), device=device, dtype=torch.uint8),
+                     torch.empty((fp8b_scale_bytes(rows, cols),), device=device, dtype=torch.uint8), fmt)
+
+
+def quant_blocks_fp8(x, fmt=FP8_E4M3, out=None):
+    """fp8-blocks quantisation of x [rows, cols] (bf16 / f32, cols % 128 == 0):
+    per 32-column block e = the smallest power of two keeping |x| / 2^(e-127)
+    <= FMT_MAX, q = rne(x 2^(127-e))."""
+    _dev(x)
+    rows, cols = x.shape
+    if out is None:
+        out = new_fp8_blocks(rows, cols, fmt, x.device)
+    _call("maeclip_quant_blocks_fp8", x.data_ptr(), _dt(x), rows, cols, x.stride(0), out.q.data_ptr(),
+          out.q.stride(0), out.e.data_ptr(), fmt, _stream())
+    return out
+
+
+def _set_q8(a, q8):
+    """maeclip_gemm_args' optional fp8-blocks copy of a bf16 output"""
+    if q8 is not None:
+        a.q8, a.ldq8, a.q8_scale, a.q8_fmt = q8.q.data_ptr(), q8.q.stride(0), q8.e.data_ptr(), q8.fmt
 
 
 def new_fp8_rows(rows, cols, fmt, device):
@@ -249,10 +296,14 @@ class Fp8WeightPlan:
               _stream())
 
 
-def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=None, aux=None, aux_out=None,
-             resid=None, colsum=None):
-    """Cout[M, N] = epilogue(alpha * (s_A[m] s_B[n]) * sum_k qA[m, k] qB[n, k]) on the
-    block-scaled fp8 MFMA (A e4m3 or e5m2, B e4m3; KC x KC, K % 128 == 0)."""
+def gemm_fp8(A, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=None, aux=None, aux_out=None,
+             resid=None, colsum=None, q8=None):
+    """Cout[M, N] = epilogue(alpha * s_B[n] * sum_k s_A qA[m, k] qB[n, k]) on the
+    block-scaled fp8 MFMA (A e4m3 or e5m2, B e4m3; KC x KC, K % 128 == 0). A is
+    an Fp8Rows (per-row s_A, applied in the epilogue) or an Fp8Blocks (e8m0
+    per 32 K, applied by the MFMA; maeclip_gemm_fp8_blocks); q8: an Fp8Blocks
+    the epilogue fills with the bf16 output's fp8 copy."""
+    blocks = isinstance(A, Fp8Blocks)
     M, K = A.q.shape
     N = B.q.shape[0]
     if B.q.shape[1] != K or B.fmt != FP8_E4M3:
@@ -265,10 +316,14 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
                    ldaux=(aux.stride(0) if aux is not None else aux_out.stride(0) if aux_out is not None else 0),
                    resid=_ptr(resid), ldr=(resid.stride(0) if resid is not None else 0),
                    colsum_partial=_ptr(colsum), splitk=1, workspace=None)
-    nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
-    if nb > 0:   # the split plan's counters + partial tiles (per stream)
-        a.workspace = _stream_scratch(A.q.device, nb).data_ptr()
-    launch = lambda: _call("maeclip_gemm_fp8", C.byref(a), A.s.data_ptr(), B.s.data_ptr(), _stream())
+    _set_q8(a, q8)
+    if blocks:
+        launch = lambda: _call("maeclip_gemm_fp8_blocks", C.byref(a), A.e.data_ptr(), B.s.data_ptr(), _stream())
+    else:
+        nb = int(L.lib().maeclip_gemm_workspace(C.byref(a)))
+        if nb > 0:   # the split plan's counters + partial tiles (per stream)
+            a.workspace = _stream_scratch(A.q.device, nb).data_ptr()
+        launch = lambda: _call("maeclip_gemm_fp8", C.byref(a), A.s.data_ptr(), B.s.data_ptr(), _stream())
     if LAUNCH_HOOK is None:
         launch()
         return Cout
@@ -279,24 +334,29 @@ def gemm_fp8(A: Fp8Rows, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=No
             nbytes += M * N * t.element_size()
     if resid is not None:
         nbytes += M * N * 4
-    key = f"M{M} N{N} K{K} KK epi{epilogue} fp8{'e5' if A.fmt == FP8_E5M2 else 'e4'}>{'bf16' if ec == 2 else 'f32'}"
+    if q8 is not None:
+        nbytes += M * N + fp8b_scale_bytes(M, N)
+    key = (f"M{M} N{N} K{K} KK epi{epilogue} fp8{'e5' if A.fmt == FP8_E5M2 else 'e4'}{'b' if blocks else ''}"
+           f">{'bf16' if ec == 2 else 'f32'}")
     LAUNCH_HOOK(key, 2.0 * M * N * K, nbytes, launch)
     return Cout
 
 
-def linear_fp8(xq: Fp8Rows, wq: Fp8Rows, bias=None, out_dtype=torch.bfloat16, epilogue=EPI_NONE, resid=None,
-               aux_out=None, aux=None, colsum=None):
+def linear_fp8(xq, wq: Fp8Rows, bias=None, out_dtype=torch.bfloat16, epilogue=EPI_NONE, resid=None,
+               aux_out=None, aux=None, colsum=None, q8=None, out=None):
     """y[M, N] = x[M, K] w[N, K]^T on fp8 operands (forward: w = W [N_out, K_in];
-    dgrad: x = dY, w = W^T [K_in, N_out])."""
-    y = torch.empty((xq.q.shape[0], wq.q.shape[0]), device=xq.q.device, dtype=out_dtype)
-    return gemm_fp8(xq, wq, y, epilogue=epilogue, bias=bias, resid=resid, aux_out=aux_out, aux=aux, colsum=colsum)
+    dgrad: x = dY, w = W^T [K_in, N_out]); xq Fp8Rows or Fp8Blocks."""
+    y = out if out is not None else torch.empty((xq.q.shape[0], wq.q.shape[0]), device=xq.q.device, dtype=out_dtype)
+    return gemm_fp8(xq, wq, y, epilogue=epilogue, bias=bias, resid=resid, aux_out=aux_out, aux=aux, colsum=colsum,
+                    q8=q8)
 
 
 def gemm_colsum_rows(M: int) -> int:
     return int(L.lib().maeclip_gemm_colsum_rows(M))
 
 
-def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, aux_out=None, colsum=None, out=None):
+def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, aux_out=None, colsum=None, out=None,
+               q8=None):
     """y[M,N] = x[M,K] w[N,K]^T (+bias) with epilogue (nn.Linear forward);
     out: an [M, N] row-major destination (e.g. a row slice of a larger buffer)."""
     M, K = x.shape
@@ -305,18 +365,18 @@ def linear_fwd(x, w, bias=None, out_dtype=None, epilogue=EPI_NONE, resid=None, a
     y = out if out is not None else torch.empty((M, N), device=x.device, dtype=out_dtype)
     gemm(x, w, y, M, N, K, x.stride(0), w.stride(0), y.stride(0), KC, KC, epilogue=epilogue, bias=bias, resid=resid,
          ldr=(resid.stride(0) if resid is not None else 0), aux_out=aux_out,
-         ldaux=(aux_out.stride(0) if aux_out is not None else 0), colsum=colsum)
+         ldaux=(aux_out.stride(0) if aux_out is not None else 0), colsum=colsum, q8=q8)
     return y
 
 
-def linear_dgrad(dy, w, out_dtype=None, epilogue=EPI_NONE, aux=None, resid=None, colsum=None, out=None):
+def linear_dgrad(dy, w, out_dtype=None, epilogue=EPI_NONE, aux=None, resid=None, colsum=None, out=None, q8=None):
     """dx[M,K] = dy[M,N] w[N,K]."""
     M, N = dy.shape
     K = w.shape[1]
     out = out if out is not None else torch.empty((M, K), device=dy.device, dtype=out_dtype or dy.dtype)
     gemm(dy, w, out, M, K, N, dy.stride(0), w.stride(0), out.stride(0), KC, RC, epilogue=epilogue, aux=aux,
          ldaux=(aux.stride(0) if aux is not None else 0), resid=resid,
-         ldr=(resid.stride(0) if resid is not None else 0), colsum=colsum)
+         ldr=(resid.stride(0) if resid is not None else 0), colsum=colsum, q8=q8)
     return out
 
 

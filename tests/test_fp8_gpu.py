@@ -121,6 +121,139 @@ def test_gemm_fp8_vs_dequantised_fp64(dev, afmt, mnk, bm, opts):
     assert (y5.double().cpu() - ref5).abs().max().item() < 1e-2 * ref5.abs().max().item()
 
 
+# ------------------------------------------------------------- fp8 blocks
+def _scale_off(r, b, T):
+    """byte offset of (row r, 32-block b) in the GEMM-layout scale tensor
+    (include/maeclip.h "fp8 blocks"), numpy restatement of common.h mc_fp8b_off"""
+    return (((r >> 6) * T + (b >> 2)) << 8) | ((b & 3) << 6) | ((r & 15) << 2) | ((r >> 4) & 3)
+
+
+def _ref_blocks(x, fmt):
+    """torch restatement of maeclip_quant_blocks_fp8: e from the bits of the
+    block amax (the smallest 2^(e-127) with amax / 2^(e-127) <= FMT_MAX), q =
+    rne(x 2^(127-e)) by torch's OCP float8 cast; returns (q bytes [rows, cols],
+    e [rows, cols / 32])"""
+    tdt, _ = F8[fmt]
+    xf = x.float().cpu()
+    rows, cols = xf.shape
+    amax = xf.abs().view(rows, cols // 32, 32).amax(-1)
+    u = amax.view(torch.int32).long()
+    e = (u >> 23) - (15 if fmt == K.FP8_E5M2 else 8) + ((u & 0x7FFFFF) > 0x600000).long()
+    e = e.clamp(min=0)
+    inv = ((254 - e) << 23).to(torch.int32).view(torch.float32)
+    q = (xf.view(rows, cols // 32, 32) * inv.unsqueeze(-1)).view(rows, cols).to(tdt)
+    return q.view(torch.uint8), e.to(torch.uint8)
+
+
+def _scales_to_rc(e_dev, rows, cols):
+    """the kernel's scale tensor -> [rows, cols / 32] (row, block) order"""
+    e = e_dev.cpu()
+    T = cols // 128
+    r = torch.arange(rows).view(-1, 1)
+    b = torch.arange(cols // 32).view(1, -1)
+    return e[_scale_off(r, b, T)]
+
+
+def _deq_blocks(op):
+    rows, cols = op.q.shape
+    tdt = F8[op.fmt][0]
+    e = _scales_to_rc(op.e, rows, cols).double()
+    return (op.q.cpu().view(tdt).double().view(rows, cols // 32, 32) * torch.pow(2.0, e - 127).unsqueeze(-1)).view(
+        rows, cols)
+
+
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(37, 512), (200, 1024), (64, 4096), (300, 640)])
+def test_quant_blocks_bit_exact(dev, fmt, dtype, shape):
+    """fp8 blocks vs the torch restatement: identical fp8 bytes and e8m0
+    exponents (at their GEMM-layout offsets); zero blocks, outliers, a 2^-20
+    .. 2^10 magnitude range; |x - 2^(e-127) q| within the format's rounding."""
+    rows, cols = shape
+    x = _rows_input(rows, cols, dtype, dev, seed=rows + cols)
+    x[7, 32:64] = 0.0
+    out = K.quant_blocks_fp8(x, fmt)
+    q_ref, e_ref = _ref_blocks(x, fmt)
+    assert torch.equal(out.q.cpu(), q_ref)
+    assert torch.equal(_scales_to_rc(out.e, rows, cols), e_ref)
+    if fmt == K.FP8_E4M3:
+        xr, xd = x.double().cpu(), _deq_blocks(out)
+        sc = torch.pow(2.0, _scales_to_rc(out.e, rows, cols).double() - 127).repeat_interleave(32, 1)
+        assert ((xd - xr).abs() <= 2.0 ** -4 * xr.abs() + sc * 2.0 ** -10 + 1e-30).all()
+
+
+@pytest.mark.parametrize("afmt", [K.FP8_E4M3, K.FP8_E5M2])
+@pytest.mark.parametrize("mnk", [(512, 384, 256), (1000, 768, 1024), (2308, 512, 2048), (9280, 1024, 512),
+                                 (18560, 1024, 4096)])
+def test_gemm_fp8_blocks_vs_dequantised_fp64(dev, afmt, mnk):
+    """fp8-blocks A (the MFMA applies the e8m0 block scales) x per-channel B:
+    vs the fp64 product of the dequantised operands (exact in fp64: only the
+    fp32 accumulation differs), with the epilogues the fp8 stack runs on it
+    (plain bf16, fp32 residual); A rows with blocks 2^30 apart in magnitude so
+    a wrong scale byte cannot hide. (18560, 1024, 4096): the C4 encoder's fc2."""
+    M, N, Kd = mnk
+    g = torch.Generator().manual_seed(M + N + 1)
+    x = torch.randn(M, Kd, generator=g) * 3
+    x[:, : Kd // 2] *= 2.0 ** -15
+    x[::7, 96:128] *= 2.0 ** 15
+    x = x.to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, Kd, generator=g) * 0.05).to(dev)
+    A = K.quant_blocks_fp8(x, afmt)
+    B = K.quant_rows_fp8(w, K.FP8_E4M3)
+    ref = _deq_blocks(A) @ _deq(B).t()
+    y = K.linear_fp8(A, B, out_dtype=torch.float32)
+    sc = ref.abs().max().item()
+    tol = 5e-6 * Kd ** 0.5
+    assert (y.double().cpu() - ref).abs().max().item() / sc < tol
+    bias = torch.randn(N, generator=g).to(dev)
+    res = torch.randn(M, N, generator=g).to(dev)
+    y2 = K.linear_fp8(A, B, bias=bias, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=res)
+    assert (y2.double().cpu() - (ref + bias.double().cpu() + res.double().cpu())).abs().max().item() < tol * sc + 1e-5
+    yb = K.linear_fp8(A, B)
+    assert (yb.double().cpu() - ref).abs().max().item() < 1e-2 * sc
+
+
+@pytest.mark.parametrize("path", ["bf16", "bf16_192", "fp8rows", "fp8blocks"])
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+def test_gemm_epilogue_fp8_blocks_output(dev, path, fmt, opts):
+    """A GEMM epilogue that writes its bf16 output's fp8 blocks itself
+    (maeclip_gemm_args q8: the fc1 GELU' and fc2-dgrad mul-aux launches of the
+    fp8 stack) gives the same bytes and exponents as maeclip_quant_blocks_fp8 of
+    the stored bf16 output: GELU' (+ aux_out), mul-aux with column sums
+    (256-row tile), plain; ragged M (a partial last tile)."""
+    M, N, Kd = 1000, 1024, 512
+    g = torch.Generator().manual_seed(17 + fmt)
+    x = (torch.randn(M, Kd, generator=g)).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, Kd, generator=g) * 0.05).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    aux = torch.rand(M, N, generator=g).to(torch.bfloat16).to(dev)
+    if path == "bf16_192":
+        opts(GEMM_BM=192)
+    if path.startswith("bf16"):
+        wb = w.to(torch.bfloat16)
+
+        def run(q8, epilogue=K.EPI_NONE, bias=None, aux=None, aux_out=None, colsum=None):
+            y = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+            K.gemm(x, wb, y, M, N, Kd, Kd, Kd, N, epilogue=epilogue, bias=bias, aux=aux, aux_out=aux_out,
+                   ldaux=N if (aux is not None or aux_out is not None) else 0, colsum=colsum, q8=q8)
+            return y
+    else:
+        A = K.quant_rows_fp8(x, K.FP8_E4M3) if path == "fp8rows" else K.quant_blocks_fp8(x, K.FP8_E4M3)
+        B = K.quant_rows_fp8(w, K.FP8_E4M3)
+        run = lambda **kw: K.linear_fp8(A, B, **kw)
+    cases = [dict(bias=bias, epilogue=K.EPI_GELU_D, aux_out=torch.empty((M, N), device=dev, dtype=torch.bfloat16)),
+             dict(epilogue=K.EPI_MUL_AUX, aux=aux), dict(bias=bias)]
+    if path != "fp8blocks":   # column sums: 256-row tiles (per-row / bf16 A only)
+        cases.append(dict(epilogue=K.EPI_MUL_AUX, aux=aux,
+                          colsum=torch.empty((K.gemm_colsum_rows(M), N), device=dev, dtype=torch.float32)))
+    for kw in cases:
+        q8 = K.new_fp8_blocks(M, N, fmt, dev)
+        y = run(q8=q8, **kw)
+        r = K.quant_blocks_fp8(y, fmt)
+        assert torch.equal(q8.q, r.q), kw.get("epilogue")
+        assert torch.equal(_scales_to_rc(q8.e, M, N), _scales_to_rc(r.e, M, N)), kw.get("epilogue")
+
+
 def test_fp8_quantisation_error_is_bounded(dev):
     """e4m3 rows: |x - s q| <= 2^-4 |x| + s 2^-10 per element (3 mantissa bits,
     RNE; subnormal step 2^-9 s) -- the operand error the fp8 GEMM adds."""
@@ -132,7 +265,8 @@ def test_fp8_quantisation_error_is_bounded(dev):
     assert ((xd - xr).abs() <= bound + 1e-12).all()
 
 
-def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
+@pytest.mark.parametrize("gfmt", ["e4m3", "e5m2"])
+def test_vitl14_336_fp8_vs_oracle_and_bf16(dev, gfmt):
     """C4 shapes (ViT-L/14 @336, encoder cut to 4 blocks, B = 4; decoder 2 x 512,
     n = 577): fp8 stack GEMMs (e4m3 forward, e5m2 x e4m3 dgrad, per-token /
     per-channel scales) and the bf16 path vs the fp64 CPU oracle (forward AND
@@ -145,11 +279,14 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
               decoder_embed_dim=512, decoder_depth=2, decoder_num_heads=16, vit_depth=4)
     batch = make_batch(4, 336)
     out = {}
+    from tests.helpers import product_config
     for prec in ("fp8", "bf16"):
-        prod, ref = build_pair(prec, **kw)
+        with product_config(fp8_grad_format=gfmt):
+            prod, ref = build_pair(prec, **kw)
         prod.eval()
-        loss = prod({k: v.to(dev) for k, v in batch.items()})
-        loss.backward()
+        with product_config(fp8_grad_format=gfmt):
+            loss = prod({k: v.to(dev) for k, v in batch.items()})
+            loss.backward()
         torch.cuda.synchronize()
         out[prec] = (loss.item(), {n: p.grad.detach().double().cpu() for n, p in prod.named_parameters()
                                    if p.requires_grad})
@@ -177,7 +314,7 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev):
     w8b, _ = worst_rel(g8, gb)
     r8 = abs(l8 - rloss) / max(1.0, abs(rloss))
     rb = abs(lb - rloss) / max(1.0, abs(rloss))
-    record_parity("vitl14_336_fp8_vs_oracle", loss_rel=r8, worst_grad_relL2=w8o, worst_grad=n8o,
+    record_parity(f"vitl14_336_fp8_vs_oracle_grad_{gfmt}", loss_rel=r8, worst_grad_relL2=w8o, worst_grad=n8o,
                   worst_grad_relL2_vs_bf16=w8b)
     record_parity("vitl14_336_bf16_vs_oracle_grads", loss_rel=rb, worst_grad_relL2=wbo, worst_grad=nbo)
     assert r8 < FP8_TOL[0], (l8, lb, rloss)
