@@ -169,7 +169,7 @@ int32_t maeclip_quant_rows_fp8(const void* x, int32_t x_dtype, int64_t rows, int
                                int64_t ldq, float* scales, int32_t fmt, void* stream);
 /* W^T quantisation (e4m3) from the fp32 master W [rows, ld]: qt [cols, ldq]
  * (ldq % 16 == 0), one scale per column of W (per row of W^T). */
-/* Every fp8 stack weight of a step at once (three launches): for each entry,
+/* Every fp8 stack weight of a step at once (two launches): for each entry,
  * q = rows of W quantised per output channel (scales sq [rows]) and qt = W^T
  * quantised per input channel (scales sqt [cols], rows of ldqt bytes), from
  * the fp32 master W [rows, ld]. The host array is filled in by
@@ -251,6 +251,16 @@ typedef struct {
   /* optional device step counter: dropout seed = seed + (*step_ptr) * MAECLIP_STEP_MULT
    * (so a captured HIP graph draws fresh masks every replay) */
   const int64_t* step_ptr;
+  /* optional fp8-blocks copy of the main output (maeclip_fp8b_scale_bytes
+   * layout; o [B*n, H*head_dim] for the forward, dqkv [B*n, 3*H*head_dim] for
+   * the backward, whose row length must be a multiple of 128): the bytes of
+   * maeclip_quant_blocks_fp8 of the bf16 output as stored. Written by the
+   * bf16 MFMA kernels' own stores; the other variants (fp32, the diagonal and
+   * row-streaming backward) run the standalone pass after the kernel. */
+  void* q8;
+  int64_t ldq8;
+  uint8_t* q8_scale;
+  int32_t q8_fmt;
 } maeclip_attn_args;
 int32_t maeclip_attn_fwd(const maeclip_attn_args* args, void* stream);
 int32_t maeclip_attn_bwd(const maeclip_attn_args* args, void* stream);

@@ -39,7 +39,8 @@ class AttnArgs(C.Structure):
                 ("key_mask", c_vp), ("colsum_partial", c_vp),
                 ("ld_qkv", c_i64), ("ld_o", c_i64), ("ld_dqkv", c_i64),
                 ("B", c_i32), ("n", c_i32), ("H", c_i32), ("head_dim", c_i32), ("dtype", c_i32),
-                ("scale", c_f32), ("dropout_p", c_f32), ("seed", c_u64), ("step_ptr", c_vp)]
+                ("scale", c_f32), ("dropout_p", c_f32), ("seed", c_u64), ("step_ptr", c_vp),
+                ("q8", c_vp), ("ldq8", c_i64), ("q8_scale", c_vp), ("q8_fmt", c_i32)]
 
 
 class LnFwdArgs(C.Structure):

@@ -66,6 +66,9 @@ text_attention_dropout = 0.1
 precision = "bf16"         # "bf16" (perf), "fp8" (C4: e4m3/e5m2 stack GEMMs, bf16 elsewhere) or "fp32" (parity mode)
 fp8_grad_format = "e4m3"   # fp8 mode: the dgrad GEMMs' gradient operand, "e4m3" (3 mantissa bits; the block / row
                            # scales give it the range) or "e5m2" (2 mantissa bits, wider range)
+# fp8 mode: the attention (forward, backward) writes its output's fp8 blocks itself, else a standalone
+# quantisation pass (A/B in DESIGN.md; MAECLIP_FP8_ATTN_Q8="10" / "11" / "00" for the A/B runs)
+fp8_attn_q8 = tuple(c == "1" for c in __import__("os").environ.get("MAECLIP_FP8_ATTN_Q8", "11")[:2])
 mask_seed = 2
 dropout_seed = 1234
 # ---- scheduling

@@ -447,11 +447,56 @@ __device__ __forceinline__ void fwd_chunk(const char* Kimg, const char* Vimg, co
   }
 }
 
+// fp8-blocks copy (maeclip_attn_args q8) of the HD columns [col0, col0 + HD)
+// of output row `row` this lane's 16-row tile stores: lane (row, g = lane / 16)
+// holds v[dt] = columns 16 dt + 4 g .. +3 as stored in bf16, so the 32-column
+// block j is dt = 2j, 2j + 1 of the four lanes l % 16 + 16 g: its amax is two
+// permlane swaps (every lane of the wave takes part; `ok` gates the stores).
+template <int HD>
+__device__ __forceinline__ void q8_store(const maeclip_attn_args& a, int64_t row, bool ok, int col0, int rowlen,
+                                         const v4f (&v)[HD / 16], int lane) {
+  const int g = lane >> 4;
+  const bool e5 = a.q8_fmt == MAECLIP_FP8_E5M2;
+#pragma unroll
+  for (int j = 0; j < HD / 32; ++j) {
+    float x[8], am = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[i] = bf2f(f2bf(v[2 * j][i]));
+      x[4 + i] = bf2f(f2bf(v[2 * j + 1][i]));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(x[i]));
+    auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+    am = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    p = __builtin_amdgcn_permlane32_swap(__float_as_uint(am), __float_as_uint(am), false, false);
+    am = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+    const unsigned ex = mc_e8m0(am, e5);
+    const float inv = mc_e8m0_inv(ex);
+    if (ok) {
+      uint8_t* q = (uint8_t*)a.q8 + row * a.ldq8 + col0 + 32 * j + 4 * g;
+      unsigned w0, w1;
+      if (e5) {
+        w0 = mc_cvt4_fp8<true>(x[0] * inv, x[1] * inv, x[2] * inv, x[3] * inv);
+        w1 = mc_cvt4_fp8<true>(x[4] * inv, x[5] * inv, x[6] * inv, x[7] * inv);
+      } else {
+        w0 = mc_cvt4_fp8<false>(x[0] * inv, x[1] * inv, x[2] * inv, x[3] * inv);
+        w1 = mc_cvt4_fp8<false>(x[4] * inv, x[5] * inv, x[6] * inv, x[7] * inv);
+      }
+      *(unsigned*)q = w0;
+      *(unsigned*)(q + 16) = w1;
+      if (g == 0) a.q8_scale[mc_fp8b_off(row, (col0 >> 5) + j, rowlen >> 7)] = (uint8_t)ex;
+    }
+  }
+}
+
 // WG = 16: up to 16 waves when the K / V images leave room for one workgroup
 // per CU only (the C4 decoder, n = 577: 37 query tiles in 3 rounds of 13
 // waves instead of 5 rounds of 8)
 template <int A, int B> constexpr int cmax() { return A > B ? A : B; }
-template <typename T, int HD, bool DROP, int WG = MAXW>
+// Q8: the fp8-blocks copy of o (maeclip_attn_args q8) from the kernel's own
+// stores -- its own instantiation, so the plain kernels keep their registers
+template <typename T, int HD, bool DROP, int WG = MAXW, bool Q8 = false>
 __global__ void __launch_bounds__(WG * 64)
 __attribute__((amdgpu_waves_per_eu(WG > MAXW ? cmax<fwd_wpe<T, HD, DROP>(), 4>() : fwd_wpe<T, HD, DROP>())))
 attn_fwd_kernel(const maeclip_attn_args a) {
@@ -521,6 +566,14 @@ attn_fwd_kernel(const maeclip_attn_args a) {
     if (std::is_same<T, bf16_t>::value && !DROP) lsum = ol[0];
     else lsum = sum4rows(lsum);
     const float inv = 1.f / lsum;
+    if constexpr (Q8 && std::is_same<T, bf16_t>::value) {
+      {
+        v4f ov[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) ov[dt] = o[dt] * inv;
+        q8_store<HD>(a, (int64_t)b * n + q, qok, h * HD, HH, ov, lane);
+      }
+    }
     if (qok) {
       T* orow = (T*)a.o + ((int64_t)b * n + q) * a.ld_o + h * HD;
 #pragma unroll
@@ -542,7 +595,7 @@ attn_fwd_kernel(const maeclip_attn_args a) {
 // two-image LDS footprint would allow three.
 // WG = 16: up to 16 waves in the one workgroup a CU holds (the C4 decoder,
 // n = 577: 37 tiles, at most 3 per wave instead of 5; register budget 128).
-template <typename T, int HD, bool TWO_ = false, int OCC = 1, int WG = MAXW>
+template <typename T, int HD, bool TWO_ = false, int OCC = 1, int WG = MAXW, bool Q8 = false>
 __global__ void __launch_bounds__(WG * 64) __attribute__((amdgpu_waves_per_eu(WG > MAXW ? 4 : 2 * OCC)))
 attn_bwd_kernel(const maeclip_attn_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -645,6 +698,15 @@ attn_bwd_kernel(const maeclip_attn_args a) {
       }
     }
     // lane holds dV[key][16dt+4g+i], dK likewise
+    if constexpr (Q8 && std::is_same<T, bf16_t>::value) {
+      {
+        v4f kv[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) kv[dt] = dk[dt] * a.scale;
+        q8_store<HD>(a, (int64_t)b * n + key, kok, HH + h * HD, 3 * HH, kv, lane);
+        q8_store<HD>(a, (int64_t)b * n + key, kok, 2 * HH + h * HD, 3 * HH, dv, lane);
+      }
+    }
     if (kok) {
       T* rowp = dqkv + (int64_t)key * a.ld_dqkv + h * HD;
 #pragma unroll
@@ -715,6 +777,14 @@ attn_bwd_kernel(const maeclip_attn_args a) {
       }
 #pragma unroll
       for (int dt = 0; dt < HD / 16; ++dt) dq[dt] = mma_rowsum<T, HD>(Ki, kc, 16 * dt, dST[0], dST[1], dq[dt], lane);
+    }
+    if constexpr (Q8 && std::is_same<T, bf16_t>::value) {
+      {
+        v4f qv[HD / 16];
+#pragma unroll
+        for (int dt = 0; dt < HD / 16; ++dt) qv[dt] = dq[dt] * a.scale;
+        q8_store<HD>(a, (int64_t)b * n + q, qok, h * HD, 3 * HH, qv, lane);
+      }
     }
     if (qok) {
       T* rowp = dqkv + (int64_t)q * a.ld_dqkv + h * HD;
@@ -1352,11 +1422,11 @@ template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)2 * npad * 4 + (size_t)nw * 3 * HD * 4;
 }
 
-template <typename T, int HD, bool TWO = false, int OCC = 1, int WG = MAXW>
+template <typename T, int HD, bool TWO = false, int OCC = 1, int WG = MAXW, bool Q8 = false>
 void launch_bwd(const maeclip_attn_args& a, dim3 grid, int nthreads, size_t lds, hipStream_t s) {
   if (lds > 65536)
-    maeclip::allow_lds((const void*)attn_bwd_kernel<T, HD, TWO, OCC, WG>, (int)lds);
-  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, TWO, OCC, WG>), grid, dim3(nthreads), lds, s, a);
+    maeclip::allow_lds((const void*)attn_bwd_kernel<T, HD, TWO, OCC, WG, Q8>, (int)lds);
+  hipLaunchKernelGGL((attn_bwd_kernel<T, HD, TWO, OCC, WG, Q8>), grid, dim3(nthreads), lds, s, a);
 }
 
 // resident workgroups per CU of a bwd variant (registers, waves and LDS)
@@ -1390,8 +1460,10 @@ int bwd_two(int n, int nw, size_t lds4, size_t lds2) {
   return c - 1;
 }
 
+// q8_done: set when the launched kernel wrote the fp8-blocks copy itself
 template <typename T, int HD>
-int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
+int run(const maeclip_attn_args& a, bool bwd, hipStream_t s, bool& q8_done) {
+  q8_done = false;
   // one wave per 16-row tile (no idle waves), at most MAXW; the forward
   // spreads its tiles evenly over the rounds it needs (n = 197: 13 tiles on 7
   // waves, not 8 waves of which 3 idle for the second round)
@@ -1450,7 +1522,9 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
       const int nw16 = tiles < 16 ? tiles : 16;
       const size_t lds16 = bwd_lds<T, HD>(a.n, nw16, true);
       if (lds16 <= 163840) {
-        launch_bwd<T, HD, true, 1, 16>(a, grid, 64 * nw16, lds16, s);
+        if (a.q8) launch_bwd<T, HD, true, 1, 16, true>(a, grid, 64 * nw16, lds16, s);
+        else launch_bwd<T, HD, true, 1, 16>(a, grid, 64 * nw16, lds16, s);
+        q8_done = a.q8 != nullptr;
         MC_CHECK_LAUNCH("maeclip_attn_bwd(16 waves)");
         return 0;
       }
@@ -1460,23 +1534,32 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s) {
     // (round 2 also had a bf16 variant that kept dS in LDS between the two
     // phases instead of recomputing S / dP for dQ: 355 vs 224 us at the
     // decoder shape, the n x n image halving the workgroups per CU; removed)
+    const bool q8 = std::is_same<T, bf16_t>::value && a.q8 != nullptr;
     if constexpr (std::is_same<T, bf16_t>::value) {
-      if (variant == 3) launch_bwd<T, HD, true, HD == 32 ? 3 : 1>(a, grid, nthreads, lds, s);
+      if (variant == 3) launch_bwd<T, HD, true, HD == 32 ? 3 : 1>(a, grid, nthreads, lds, s);   // (no q8: pass)
+      else if (two && q8) launch_bwd<T, HD, true, 1, MAXW, true>(a, grid, nthreads, lds, s);
       else if (two) launch_bwd<T, HD, true>(a, grid, nthreads, lds, s);
+      else if (q8) launch_bwd<T, HD, false, 1, MAXW, true>(a, grid, nthreads, lds, s);
+      q8_done = q8 && variant != 3;
     }
-    if (!two) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
+    if (!two && !q8) launch_bwd<T, HD, false>(a, grid, nthreads, lds, s);
   } else {
-    auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true> : attn_fwd_kernel<T, HD, false>;
+    // the fused fp8 copy: bf16 without dropout (the fp8 stacks' case)
+    const bool q8 = std::is_same<T, bf16_t>::value && a.q8 != nullptr && a.dropout_p == 0.f;
+    auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true>
+                                  : (q8 ? attn_fwd_kernel<T, HD, false, MAXW, true> : attn_fwd_kernel<T, HD, false>);
     int nth = nthreads;
     // one workgroup per CU by LDS and more tiles than MAXW waves: up to 16
     // waves (option ATTN_FW16 = 0 turns it off)
     if (tiles > MAXW && 2 * lds > 163840 && maeclip::option(MAECLIP_OPT_ATTN_FW16, 1) != 0) {
       const int r16 = (tiles + 15) / 16;
       nth = 64 * ((tiles + r16 - 1) / r16);
-      kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true, 16> : attn_fwd_kernel<T, HD, false, 16>;
+      kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true, 16>
+                               : (q8 ? attn_fwd_kernel<T, HD, false, 16, true> : attn_fwd_kernel<T, HD, false, 16>);
     }
     if (lds > 65536) maeclip::allow_lds((const void*)kern, (int)lds);
     hipLaunchKernelGGL(kern, grid, dim3(nth), lds, s, a);
+    q8_done = q8;
   }
   MC_CHECK_LAUNCH(bwd ? "maeclip_attn_bwd" : "maeclip_attn_fwd");
   return 0;
@@ -1493,15 +1576,31 @@ int check(const maeclip_attn_args* a, bool bwd) {
     MC_CHECK_ARG(a->dout && a->dqkv && a->lse, "maeclip_attn_bwd: null pointer");
     MC_CHECK_ARG(a->ld_dqkv % epc == 0, "maeclip_attn_bwd: ld_dqkv");
   }
+  if (a->q8) {
+    const int64_t len = (int64_t)a->H * a->head_dim * (bwd ? 3 : 1);
+    MC_CHECK_ARG(len % 128 == 0 && a->ldq8 >= len && a->ldq8 % 16 == 0 && ((uintptr_t)a->q8 & 15) == 0 &&
+                     a->q8_scale && (a->q8_fmt == MAECLIP_FP8_E4M3 || a->q8_fmt == MAECLIP_FP8_E5M2),
+                 "maeclip_attn: fp8-blocks output needs a row length %% 128, ldq8 %% 16, a scale buffer and a format");
+  }
   return 0;
 }
 
 int dispatch(const maeclip_attn_args* a, bool bwd, void* stream) {
   if (int e = check(a, bwd)) return e;
   hipStream_t s = (hipStream_t)stream;
+  bool q8_done = false;
+  int rc;
   if (a->dtype == MAECLIP_BF16)
-    return a->head_dim == 64 ? run<bf16_t, 64>(*a, bwd, s) : run<bf16_t, 32>(*a, bwd, s);
-  return a->head_dim == 64 ? run<float, 64>(*a, bwd, s) : run<float, 32>(*a, bwd, s);
+    rc = a->head_dim == 64 ? run<bf16_t, 64>(*a, bwd, s, q8_done) : run<bf16_t, 32>(*a, bwd, s, q8_done);
+  else
+    rc = a->head_dim == 64 ? run<float, 64>(*a, bwd, s, q8_done) : run<float, 32>(*a, bwd, s, q8_done);
+  if (rc != 0 || !a->q8 || q8_done) return rc;
+  // variants without the fused copy: the standalone pass over the output
+  const int64_t HH = (int64_t)a->H * a->head_dim;
+  return bwd ? maeclip_quant_blocks_fp8(a->dqkv, a->dtype, (int64_t)a->B * a->n, 3 * HH, a->ld_dqkv, a->q8, a->ldq8,
+                                        a->q8_scale, a->q8_fmt, stream)
+             : maeclip_quant_blocks_fp8(a->o, a->dtype, (int64_t)a->B * a->n, HH, a->ld_o, a->q8, a->ldq8,
+                                        a->q8_scale, a->q8_fmt, stream);
 }
 
 }  // namespace

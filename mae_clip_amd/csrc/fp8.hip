@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256) quant_cols_kernel(const float* __restrict
   }
 }
 
-// ---- all stack weights of a step in three launches (maeclip_quant_weights_fp8)
+// ---- all stack weights of a step in two launches (maeclip_quant_weights_fp8)
 // entry lookup: the last entry whose prefix start is <= u (n <= a few hundred)
 __device__ __forceinline__ int wentry(const maeclip_fp8w_entry* __restrict__ e, int n, int64_t u, bool strips) {
   int lo = 0, hi = n - 1;
@@ -194,10 +194,10 @@ __device__ __forceinline__ int wentry(const maeclip_fp8w_entry* __restrict__ e, 
 }
 
 // W rows (per output channel): one wave per row of the concatenated row space
-__global__ void __launch_bounds__(256) wq_rows_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
-                                                      int64_t total_rows) {
+__device__ __forceinline__ void wq_rows(const maeclip_fp8w_entry* __restrict__ e, int n, int64_t total_rows,
+                                        int64_t blk) {
   const int lane = threadIdx.x & 63;
-  const int64_t grow = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t grow = blk * 4 + (threadIdx.x >> 6);
   if (grow >= total_rows) return;
   const maeclip_fp8w_entry& w = e[wentry(e, n, grow, false)];
   const int64_t r = grow - w.row_begin;
@@ -227,10 +227,8 @@ __global__ void __launch_bounds__(256) wq_rows_kernel(const maeclip_fp8w_entry* 
 }
 
 // W^T: units = (entry, 64-column strip, 256-row chunk), chunk fastest
-__global__ void __launch_bounds__(256) wq_cols_amax_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
-                                                           float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int64_t gu = blockIdx.x;
+__device__ __forceinline__ void wq_cols_amax(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                             float* __restrict__ part, int64_t gu, float (&red)[4][64]) {
   const maeclip_fp8w_entry& w = e[wentry(e, n, gu, true)];
   const int lu = (int)(gu - w.unit_begin), nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
   const int c0 = (lu / nch) * 64, r0 = (lu % nch) * QC_ROWS;
@@ -243,6 +241,16 @@ __global__ void __launch_bounds__(256) wq_cols_amax_kernel(const maeclip_fp8w_en
   if (tr == 0 && col < w.cols)
     part[w.part_begin + (int64_t)(lu % nch) * w.cols + col] =
         fmaxf(fmaxf(red[0][tc], red[1][tc]), fmaxf(red[2][tc], red[3][tc]));
+}
+
+// one launch for both independent first passes: workgroups [0, rows_blocks)
+// quantise W rows, the rest take the partial column maxima of W^T
+__global__ void __launch_bounds__(256) wq_rows_amax_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                                           int64_t total_rows, int64_t rows_blocks,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4][64];
+  if ((int64_t)blockIdx.x < rows_blocks) wq_rows(e, n, total_rows, blockIdx.x);
+  else wq_cols_amax(e, n, part, (int64_t)blockIdx.x - rows_blocks, red);
 }
 
 __global__ void __launch_bounds__(256) wq_cols_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
@@ -396,10 +404,9 @@ extern "C" int32_t maeclip_quant_weights_fp8(const maeclip_fp8w_entry* dev, cons
   }
   MC_CHECK_ARG(workspace && ws_bytes >= part * 4, "maeclip_quant_weights_fp8: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wq_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, dev, n, rows);
-  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(rows)");
-  hipLaunchKernelGGL(wq_cols_amax_kernel, dim3((unsigned)units), dim3(256), 0, s, dev, n, workspace);
-  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(cols amax)");
+  const int64_t rb = (rows + 3) / 4;
+  hipLaunchKernelGGL(wq_rows_amax_kernel, dim3((unsigned)(rb + units)), dim3(256), 0, s, dev, n, rows, rb, workspace);
+  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(rows + cols amax)");
   hipLaunchKernelGGL(wq_cols_kernel, dim3((unsigned)units), dim3(256), 0, s, dev, n, (const float*)workspace);
   MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(cols)");
   return 0;

@@ -185,6 +185,13 @@ def _b8(f8, M, D, fmt, dev):
     return K.new_fp8_blocks(M, D, fmt, dev) if f8 is not None else None
 
 
+def _attn_q8(f8, M, D, fmt, dev, bwd):
+    """Fp8Blocks for the attention to fill (config.fp8_attn_q8), else None (the
+    consumer GEMM's operand is then made by a standalone pass)"""
+    from . import config as CFG
+    return _b8(f8, M, D, fmt, dev) if CFG.fp8_attn_q8[1 if bwd else 0] else None
+
+
 def _q8(f8, M, D, fmt, dev):
     """Fp8Rows for a LayerNorm to fill when its consumer GEMM runs in fp8."""
     return K.new_fp8_rows(M, D, fmt, dev) if f8 is not None else None
@@ -274,15 +281,16 @@ def microbatch_active():
 
 
 def microbatch_count(spec) -> int:
-    """Micro-batches for a stack: CFG.stack_microbatches on the bf16 path
-    (fp8 and fp32 parity mode run one), when every micro-batch keeps whole
-    64-row groups of the GEMM column-sum partials."""
+    """Micro-batches for a stack: CFG.stack_microbatches on the bf16 and fp8
+    paths (the fp32 parity mode runs one), when every micro-batch keeps whole
+    64-row groups of the GEMM column-sum partials (and of the fp8 blocks'
+    scale layout)."""
     from . import config as CFG
     import os
     S = int(getattr(CFG, "stack_microbatches", 1) or 1)
     # A/B scans only: MAECLIP_MB_D<width> overrides the count for stacks of that width
     S = int(os.environ.get(f"MAECLIP_MB_D{spec.D}", S))
-    if S <= 1 or spec.dtype != torch.bfloat16 or spec.w8 is not None or spec.B % S:
+    if S <= 1 or spec.dtype != torch.bfloat16 or spec.B % S:
         return 1
     return S if (spec.B // S * spec.n) % 64 == 0 else 1
 
@@ -309,8 +317,10 @@ class TransformerStackFn(torch.autograd.Function):
             h1, m1, r1, _, _ = K.ln_fwd(xi, n1w, n1b, spec.eps, out_dtype=T, q8=q1)
             qkv = _fwd(h1, wqkv, f8[0], xq=q1, bias=bqkv)
             del q1
-            o, lse = K.attn_fwd(qkv, B, n, H, hd, scale)
-            x1 = _fwd(o, wproj, f8[1], bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
+            o8 = _attn_q8(f8[1], M, D, K.FP8_E4M3, dev, False)   # the proj GEMM's fp8 operand
+            o, lse = K.attn_fwd(qkv, B, n, H, hd, scale, q8=o8)
+            x1 = _fwd(o, wproj, f8[1], xq=o8, bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xi)
+            del o8
             q2 = _q8(f8[2], M, D, K.FP8_E4M3, dev)
             h2, m2, r2, _, _ = K.ln_fwd(x1, n2w, n2b, spec.eps, out_dtype=T, q8=q2)
             # fc1 epilogue: a = gelu(h), dgelu = gelu'(h) saved for the backward
@@ -353,27 +363,34 @@ class TransformerStackFn(torch.autograd.Function):
         xin = [xi[slice(r0, r1)] for r0, r1 in mb.rows]
         # block by block, each micro-batch's launches on its stream in turn (the
         # captured graph then holds S interleaved chains the replay overlaps)
+        Ms = M // S
         for i, (wqkv, wproj, w1, w2) in enumerate(spec.wT):
             p = params[i * PER_BLOCK:(i + 1) * PER_BLOCK]
             n1w, n1b, _, bqkv, _, bproj, n2w, n2b, _, b1, _, b2 = p
             _, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = saved[i]
+            f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
             for mi, rs, bs in mb.each():
                 xr = xin[mi]
-                K.ln_fwd(xr, n1w, n1b, spec.eps, out_dtype=T, y_out=h1[rs], mean_out=m1[rs], rstd_out=r1[rs])
+                # fp8 mode: each micro-batch's fp8 operands (LayerNorm rows, fc1's blocks)
+                q1 = _q8(f8[0], Ms, D, K.FP8_E4M3, dev)
+                K.ln_fwd(xr, n1w, n1b, spec.eps, out_dtype=T, y_out=h1[rs], mean_out=m1[rs], rstd_out=r1[rs], q8=q1)
                 mb.tick()
-                K.linear_fwd(h1[rs], wqkv, bias=bqkv, out=qkv[rs])
+                _fwd(h1[rs], wqkv, f8[0], xq=q1, bias=bqkv, out=qkv[rs])
                 mb.tick()
-                K.attn_fwd(qkv[rs], mb.Bs, n, H, hd, scale, o_out=o[rs], lse_out=lse[bs])
+                o8 = _attn_q8(f8[1], Ms, D, K.FP8_E4M3, dev, False)
+                K.attn_fwd(qkv[rs], mb.Bs, n, H, hd, scale, o_out=o[rs], lse_out=lse[bs], q8=o8)
                 mb.tick()
-                K.linear_fwd(o[rs], wproj, bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xr,
-                             out=x1[rs])
+                _fwd(o[rs], wproj, f8[1], xq=o8, bias=bproj, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=xr,
+                     out=x1[rs])
                 mb.tick()
-                K.ln_fwd(x1[rs], n2w, n2b, spec.eps, out_dtype=T, y_out=h2[rs], mean_out=m2[rs], rstd_out=r2[rs])
+                q2 = _q8(f8[2], Ms, D, K.FP8_E4M3, dev)
+                K.ln_fwd(x1[rs], n2w, n2b, spec.eps, out_dtype=T, y_out=h2[rs], mean_out=m2[rs], rstd_out=r2[rs], q8=q2)
                 mb.tick()
-                K.linear_fwd(h2[rs], w1, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu[rs], out=a[rs])
+                a8 = _b8(f8[3], Ms, w1.shape[0], K.FP8_E4M3, dev)
+                _fwd(h2[rs], w1, f8[2], xq=q2, q8=a8, bias=b1, epilogue=K.EPI_GELU_D, aux_out=dgelu[rs], out=a[rs])
                 mb.tick()
-                K.linear_fwd(a[rs], w2, bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1[rs],
-                             out=outs[i][rs])
+                _fwd(a[rs], w2, f8[3], xq=a8, bias=b2, out_dtype=torch.float32, epilogue=K.EPI_RESID, resid=x1[rs],
+                     out=outs[i][rs])
                 xin[mi] = outs[i][rs]
         mb.join()
         for i in range(len(spec.wT)):
@@ -442,10 +459,12 @@ class TransformerStackFn(torch.autograd.Function):
             del q1
             gi[4] = wq.wgrad(dx1T, o, out=gout(ar, p[4]))
             # attention
-            dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale)
+            dq8 = _attn_q8(f8[0], M, 3 * D, _gfmt(), g.device, True)   # the qkv dgrad's fp8 operand
+            dqkv, qpart = K.attn_bwd(qkv, o, dO, lse, B, n, H, hd, scale, q8=dq8)
             del dO
             gi[3] = rb.add(qpart, out=gout(ar, p[3]))
-            dh1 = _dgrad(dqkv, wqkv, f8[0])
+            dh1 = _dgrad(dqkv, wqkv, f8[0], dyq=dq8)
+            del dq8
             gi[2] = wq.wgrad(dqkv, h1, out=gout(ar, p[2]))
             del dqkv
             # norm1 (+ residual gradient)
@@ -499,36 +518,44 @@ class TransformerStackFn(torch.autograd.Function):
                              dh1=e((M, D)), dx=e((M, D), f32), dxT=e((M, D)), pg1=e((S * G, D), f32),
                              pb1=e((S * G, D), f32), pc1=e((S * G, D), f32)))
         mb.fork()
-        gin = [(g[slice(r0, r1)], gT[slice(r0, r1)]) for r0, r1 in mb.rows]
+        # per micro-batch: (f32 residual gradient, its bf16 copy, the copy's fp8
+        # rows from the LayerNorm backward that made it -- fp8 mode)
+        gin = [(g[slice(r0, r1)], gT[slice(r0, r1)], None) for r0, r1 in mb.rows]
         for i in reversed(range(len(spec.wT))):
             wqkv, wproj, w1, w2 = spec.wT[i]
             n1w, n2w = params[i * PER_BLOCK], params[i * PER_BLOCK + 6]
             xi, h1, m1, r1, qkv, o, lse, x1, h2, m2, r2, dgelu, a = ctx.saved[i]
             b = bufs[i]
+            f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
+            f8n = spec.w8[i - 1][3] if spec.w8 is not None and i > 0 else None
             for mi, rs, bs in mb.each():
-                gs, gTs = gin[mi]
+                gs, gTs, gq = gin[mi]
                 ps = slice(mi * G, (mi + 1) * G)
                 cs = slice(rs.start // 64, rs.stop // 64)
-                K.linear_dgrad(gTs, w2, epilogue=K.EPI_MUL_AUX, aux=dgelu[rs], colsum=b["dA_part"][cs],
-                               out=b["dA"][rs])
+                dA8 = _b8(f8[2], Ms, w1.shape[0], _gfmt(), dev)
+                _dgrad(gTs, w2, f8[3], dyq=gq, q8=dA8, epilogue=K.EPI_MUL_AUX, aux=dgelu[rs],
+                       colsum=b["dA_part"][cs], out=b["dA"][rs])
                 mb.tick()
-                K.linear_dgrad(b["dA"][rs], w1, out=b["dh2"][rs])
+                _dgrad(b["dA"][rs], w1, f8[2], dyq=dA8, out=b["dh2"][rs])
                 mb.tick()
+                q1 = _q8(f8[1], Ms, D, _gfmt(), dev)
                 K.ln_bwd(b["dh2"][rs], x1[rs], m2[rs], r2[rs], n2w, dres=gs, want_bf16=True, want_colsum=True,
                          dx_out=b["dx1"][rs], dxb_out=b["dx1T"][rs], pg_out=b["pg2"][ps], pb_out=b["pb2"][ps],
-                         pc_out=b["pc2"][ps])
+                         pc_out=b["pc2"][ps], q8=q1)
                 mb.tick()
-                K.linear_dgrad(b["dx1T"][rs], wproj, out=b["dO"][rs])
+                _dgrad(b["dx1T"][rs], wproj, f8[1], dyq=q1, out=b["dO"][rs])
                 mb.tick()
+                dq8 = _attn_q8(f8[0], Ms, 3 * D, _gfmt(), dev, True)
                 K.attn_bwd(qkv[rs], o[rs], b["dO"][rs], lse[bs], mb.Bs, n, H, hd, scale,
-                           dqkv_out=b["dqkv"][rs], part_out=b["qpart"][bs])
+                           dqkv_out=b["dqkv"][rs], part_out=b["qpart"][bs], q8=dq8)
                 mb.tick()
-                K.linear_dgrad(b["dqkv"][rs], wqkv, out=b["dh1"][rs])
+                _dgrad(b["dqkv"][rs], wqkv, f8[0], dyq=dq8, out=b["dh1"][rs])
                 mb.tick()
+                gq = _q8(f8n, Ms, D, _gfmt(), dev)
                 K.ln_bwd(b["dh1"][rs], xi[rs], m1[rs], r1[rs], n1w, dres=b["dx1"][rs], want_bf16=True,
                          want_colsum=True, dx_out=b["dx"][rs], dxb_out=b["dxT"][rs], pg_out=b["pg1"][ps],
-                         pb_out=b["pb1"][ps], pc_out=b["pc1"][ps])
-                gin[mi] = (b["dx"][rs], b["dxT"][rs])
+                         pb_out=b["pb1"][ps], pc_out=b["pc1"][ps], q8=gq)
+                gin[mi] = (b["dx"][rs], b["dxT"][rs], gq)
         mb.join()
         ar = ctx.arena
         for i in reversed(range(len(spec.wT))):

@@ -267,7 +267,7 @@ def quant_cols_fp8(w, out=None):
 
 class Fp8WeightPlan:
     """fp8 operands of a set of fp32 GEMM weights W [N, K], refreshed for all of
-    them in one maeclip_quant_weights_fp8 call (three launches): W per output
+    them in one maeclip_quant_weights_fp8 call (two launches): W per output
     channel (forward B operand) and W^T per input channel (dgrad B operand)."""
 
     def __init__(self, weights, device):
@@ -555,7 +555,9 @@ def ln_bwd(dy, x, mean, rstd, gamma, dres=None, want_bf16=False, want_param_grad
 
 # -------------------------------------------------------------- attention
 def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want_lse=True, step_ptr=None,
-             o_out=None, lse_out=None):
+             o_out=None, lse_out=None, q8=None):
+    """(o, lse); q8 (Fp8Blocks [B*n, H*hd], optional): also filled with the fp8
+    blocks of o as stored (the proj GEMM's operand in fp8 mode)."""
     _dev(qkv, key_mask)
     D = H * hd
     o = o_out if o_out is not None else torch.empty((B * n, D), device=qkv.device, dtype=qkv.dtype)
@@ -566,11 +568,15 @@ def attn_fwd(qkv, B, n, H, hd, scale, key_mask=None, dropout_p=0.0, seed=0, want
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=_ptr(lse), dout=None, dqkv=None, key_mask=_ptr(key_mask),
                    colsum_partial=None, ld_qkv=qkv.stride(0), ld_o=D, ld_dqkv=0, B=B, n=n, H=H, head_dim=hd,
                    dtype=_dt(qkv), scale=scale, dropout_p=dropout_p, seed=int(seed), step_ptr=_ptr(step_ptr))
+    _set_q8(a, q8)
     _call("maeclip_attn_fwd", C.byref(a), _stream())
     return o, lse
 
 
-def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=None, dqkv_out=None, part_out=None):
+def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=None, dqkv_out=None, part_out=None,
+             q8=None):
+    """(dqkv, bias-gradient partials); q8 (Fp8Blocks [B*n, 3*H*hd], optional):
+    the fp8 blocks of dqkv as stored (the qkv dgrad GEMM's operand)."""
     _dev(qkv, o, dout, lse, key_mask)
     D = H * hd
     dqkv = dqkv_out if dqkv_out is not None else torch.empty((B * n, 3 * D), device=qkv.device, dtype=qkv.dtype)
@@ -581,6 +587,7 @@ def attn_bwd(qkv, o, dout, lse, B, n, H, hd, scale, want_colsum=True, key_mask=N
     a = L.AttnArgs(qkv=qkv.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(), dout=dout.data_ptr(), dqkv=dqkv.data_ptr(),
                    key_mask=_ptr(key_mask), colsum_partial=_ptr(part), ld_qkv=qkv.stride(0), ld_o=o.stride(0),
                    ld_dqkv=3 * D, B=B, n=n, H=H, head_dim=hd, dtype=_dt(qkv), scale=scale, dropout_p=0.0, seed=0)
+    _set_q8(a, q8)
     _call("maeclip_attn_bwd", C.byref(a), _stream())
     return dqkv, part
 

@@ -254,6 +254,31 @@ def test_gemm_epilogue_fp8_blocks_output(dev, path, fmt, opts):
         assert torch.equal(_scales_to_rc(q8.e, M, N), _scales_to_rc(r.e, M, N)), kw.get("epilogue")
 
 
+@pytest.mark.parametrize("shape", [(2, 145, 4, 64), (2, 50, 2, 64), (3, 197, 4, 32), (1, 577, 4, 32), (2, 197, 2, 64)])
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+def test_attention_fp8_blocks_output(dev, shape, fmt):
+    """The attention forward / backward write the fp8 blocks of o / dqkv (the
+    proj forward's and the qkv dgrad's fp8 operands) from their own stores:
+    the same bytes and exponents as maeclip_quant_blocks_fp8 of the bf16
+    output. (145, hd 64): the C4 encoder; (197, hd 32): the diagonal backward,
+    which takes the standalone pass; (577, hd 32): the 16-wave kernels."""
+    B, n, H, hd = shape
+    g = torch.Generator().manual_seed(n + H)
+    qkv = (torch.randn(B * n, 3 * H * hd, generator=g)).to(torch.bfloat16).to(dev)
+    D = H * hd
+    q8 = K.new_fp8_blocks(B * n, D, fmt, dev)
+    o, lse = K.attn_fwd(qkv, B, n, H, hd, hd ** -0.5, q8=q8)
+    r = K.quant_blocks_fp8(o, fmt)
+    assert torch.equal(q8.q, r.q)
+    assert torch.equal(_scales_to_rc(q8.e, B * n, D), _scales_to_rc(r.e, B * n, D))
+    dout = (torch.randn(B * n, D, generator=g) * 1e-2).to(torch.bfloat16).to(dev)
+    d8 = K.new_fp8_blocks(B * n, 3 * D, fmt, dev)
+    dqkv, _ = K.attn_bwd(qkv, o, dout, lse, B, n, H, hd, hd ** -0.5, q8=d8)
+    r = K.quant_blocks_fp8(dqkv, fmt)
+    assert torch.equal(d8.q, r.q)
+    assert torch.equal(_scales_to_rc(d8.e, B * n, 3 * D), _scales_to_rc(r.e, B * n, 3 * D))
+
+
 def test_fp8_quantisation_error_is_bounded(dev):
     """e4m3 rows: |x - s q| <= 2^-4 |x| + s 2^-10 per element (3 mantissa bits,
     RNE; subnormal step 2^-9 s) -- the operand error the fp8 GEMM adds."""
@@ -328,7 +353,7 @@ BF16_C4_TOL = 1.25e-2           # measured r03: 0.0061
 
 
 def test_batched_weight_quantisation_matches_single(dev):
-    """maeclip_quant_weights_fp8 (all stack weights in three launches) ==
+    """maeclip_quant_weights_fp8 (all stack weights in two launches) ==
     the per-weight quant_rows_fp8 / quant_cols_fp8, bit for bit, over weights of
     different shapes (row counts not multiples of 64 / 256)."""
     g = torch.Generator().manual_seed(3)

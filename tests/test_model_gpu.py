@@ -647,9 +647,10 @@ def test_uint8_pixel_batch_equals_normalised_batch(dev, precision, mask_ratio):
         assert torch.equal(gr, out[1][1][n]), n
 
 
-def test_stack_microbatches_match_whole_batch(dev, opts):
-    """config.stack_microbatches = 2 (the bf16 stacks' samples split into two
-    chains on two streams, functions.MicroBatches) == one chain: identical
+@pytest.mark.parametrize("precision", ["bf16", "fp8"])
+def test_stack_microbatches_match_whole_batch(dev, opts, precision):
+    """config.stack_microbatches = 2 (the bf16 / fp8 stacks' samples split into
+    two chains on two streams, functions.MicroBatches) == one chain: identical
     loss and bitwise-identical weight gradients (every GEMM / LayerNorm /
     attention row is computed the same way; the weight gradients run once on
     the whole-batch buffers); bias and LayerNorm parameter gradients, whose
@@ -669,7 +670,7 @@ def test_stack_microbatches_match_whole_batch(dev, opts):
     res = {}
     batch = {k: v.to(dev) for k, v in make_batch(128, 224, seed=5).items()}
     for S in (1, 2):
-        with product_config(precision="bf16", stack_microbatches=S, **kw):
+        with product_config(precision=precision, stack_microbatches=S, **kw):
             torch.manual_seed(0)
             m = CLIPModel().to(dev).eval()
             spec_s = Fn.microbatch_count(Fn.StackSpec(B=128, n=50, D=768, H=12, eps=1e-6, dtype=torch.bfloat16, wT=[]))
@@ -689,7 +690,7 @@ def test_stack_microbatches_match_whole_batch(dev, opts):
             e = ((a - b).norm() / (a.norm() + 1e-30)).item()
             worst = max(worst, e)
             assert e < 1e-5, (n, e)
-    record_parity("stack_microbatches_2_vs_1", worst_bias_ln_grad_relL2=worst)
+    record_parity(f"stack_microbatches_2_vs_1_{precision}", worst_bias_ln_grad_relL2=worst)
 
 
 @pytest.mark.parametrize("sk", [0, 1])
