@@ -293,12 +293,13 @@ def test_fp8_quantisation_error_is_bounded(dev):
 @pytest.mark.parametrize("gfmt", ["e4m3", "e5m2"])
 def test_vitl14_336_fp8_vs_oracle_and_bf16(dev, gfmt):
     """C4 shapes (ViT-L/14 @336, encoder cut to 4 blocks, B = 4; decoder 2 x 512,
-    n = 577): fp8 stack GEMMs (e4m3 forward, e5m2 x e4m3 dgrad, per-token /
-    per-channel scales) and the bf16 path vs the fp64 CPU oracle (forward AND
-    backward) on the same weights. Tolerances (about 2x the values measured on
-    MI355X, profiles/r03/parity.json): loss relative FP8_TOL[0]; every
-    trainable gradient's relative L2 error vs the ORACLE's within FP8_TOL[1]
-    (bf16: BF16_C4_TOL); fp8 vs bf16 within FP8_TOL[2]."""
+    n = 577): fp8 stack GEMMs (e4m3 forward; the gradient operand in e4m3, the
+    default, or e5m2; per-token scales from the LayerNorms, fp8 blocks from the
+    GEMM epilogues and the attention, per-channel weight scales) and the bf16
+    path vs the fp64 CPU oracle (forward AND backward) on the same weights.
+    Tolerances FP8_TOL_BY_FMT (about 2x the values measured on MI355X): loss
+    relative; every trainable gradient's relative L2 error vs the ORACLE's (bf16:
+    BF16_C4_TOL); fp8 vs bf16."""
     from tests.helpers import record_parity
     kw = dict(model_name="vit_large_patch14_336", size=336, image_embedding=1024, text_layers=2, mask_ratio=0.75,
               decoder_embed_dim=512, decoder_depth=2, decoder_num_heads=16, vit_depth=4)
@@ -342,13 +343,17 @@ def test_vitl14_336_fp8_vs_oracle_and_bf16(dev, gfmt):
     record_parity(f"vitl14_336_fp8_vs_oracle_grad_{gfmt}", loss_rel=r8, worst_grad_relL2=w8o, worst_grad=n8o,
                   worst_grad_relL2_vs_bf16=w8b)
     record_parity("vitl14_336_bf16_vs_oracle_grads", loss_rel=rb, worst_grad_relL2=wbo, worst_grad=nbo)
-    assert r8 < FP8_TOL[0], (l8, lb, rloss)
-    assert w8o < FP8_TOL[1], (w8o, n8o)
+    tol = FP8_TOL_BY_FMT[gfmt]
+    assert r8 < tol[0], (l8, lb, rloss)
+    assert w8o < tol[1], (w8o, n8o)
     assert wbo < BF16_C4_TOL, (wbo, nbo)
-    assert w8b < FP8_TOL[2], w8b
+    assert w8b < tol[2], w8b
 
 
-FP8_TOL = (2.5e-2, 0.2, 0.2)     # measured r03: 0.0121 (0.0075 on earlier r03 builds: fp8 rounding noise), 0.108, 0.108
+# (loss rel, worst grad rel-L2 vs the oracle, vs bf16) per gradient format, about 2x
+# the measurements (r06, fp8 blocks + per-row operands: e4m3 0.0115 / 0.082 / 0.082,
+# e5m2 0.0115 / 0.110 / 0.111; profiles/r06/parity_r6d.jsonl)
+FP8_TOL_BY_FMT = {"e4m3": (2.5e-2, 0.16, 0.16), "e5m2": (2.5e-2, 0.2, 0.2)}
 BF16_C4_TOL = 1.25e-2           # measured r03: 0.0061
 
 
