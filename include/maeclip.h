@@ -362,6 +362,10 @@ int32_t maeclip_colsum_multi(const maeclip_colsum_entry* dev_entries, const maec
  * out_bf16 [M, D]. */
 int32_t maeclip_rows_colsum(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld, void* out_bf16,
                             float* partial, void* stream);
+/* the same with the fp8 rows of the bf16 copy (per-row scales, bit-identical
+ * to maeclip_quant_rows_fp8 of out_bf16; the fp8 stack's top operand) */
+int32_t maeclip_rows_colsum_q8(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld, void* out_bf16,
+                               float* partial, void* q8, int64_t ldq8, float* q8_scale, int32_t q8_fmt, void* stream);
 int32_t maeclip_rows_colsum_partial_rows(int64_t M);
 /* timm global_pool="avg": out[b] = mean_{t>=1} x[b,t,:] ; bwd scatters 1/(n-1) */
 int32_t maeclip_pool_fwd(const float* x, int32_t B, int32_t n, int32_t D, float* out, void* stream);

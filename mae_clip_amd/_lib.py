@@ -177,6 +177,7 @@ _SIGS = {
     "maeclip_colsum_reduce": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_f32, c_vp, c_vp]),
     "maeclip_rows_colsum": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "maeclip_rows_colsum_partial_rows": (c_i32, [c_i64]),
+    "maeclip_rows_colsum_q8": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp]),
     "maeclip_colsum_scratch": (c_i64, [c_i64, c_i64]),
     "maeclip_cast_flat": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_i64, c_f32, c_vp]),
     "maeclip_pool_fwd": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp]),

@@ -146,15 +146,21 @@ __global__ void __launch_bounds__(NTH) embed_kernel(const int64_t* __restrict__ 
 // colsum partials of a row matrix (bias gradient of a Linear whose output
 // gradient arrives un-reduced), optionally emitting a bf16 copy of the rows.
 constexpr int RC_MAXC = 8;  // D <= 2048
-template <typename T>
+// Q8 (with out_bf): also the fp8 rows of the bf16 copy, bit-identical to
+// maeclip_quant_rows_fp8 of it (the fp8 stack's top fc2-dgrad operand)
+template <typename T, bool Q8 = false>
 __global__ void __launch_bounds__(NTH) rows_colsum_kernel(const T* __restrict__ x, int64_t M, int D, int64_t ld,
-                                                          bf16_t* __restrict__ out_bf, float* __restrict__ partial) {
+                                                          bf16_t* __restrict__ out_bf, float* __restrict__ partial,
+                                                          uint8_t* __restrict__ q8 = nullptr, int64_t ldq8 = 0,
+                                                          float* __restrict__ q8_scale = nullptr, bool e5 = false) {
   __shared__ float red[NTH / 64][RC_MAXC * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float acc[RC_MAXC][4];
 #pragma unroll
   for (int c = 0; c < RC_MAXC; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = 0.f;
   for (int64_t r = (int64_t)blockIdx.x * (NTH / 64) + wave; r < M; r += (int64_t)gridDim.x * (NTH / 64)) {
+    float rv[Q8 ? RC_MAXC : 1][4];
+    float amax = 0.f;
 #pragma unroll
     for (int c = 0; c < RC_MAXC; ++c) {
       const int e = c * 256 + lane * 4;
@@ -162,8 +168,18 @@ __global__ void __launch_bounds__(NTH) rows_colsum_kernel(const T* __restrict__ 
         const v4f v = ld4<T>(x + r * ld + e);
         acc[c][0] += v[0]; acc[c][1] += v[1]; acc[c][2] += v[2]; acc[c][3] += v[3];
         if (out_bf) st4<bf16_t>(out_bf + r * D + e, v);
+        if constexpr (Q8) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            rv[c][j] = bf2f(f2bf(v[j]));
+            amax = fmaxf(amax, fabsf(rv[c][j]));
+          }
+        }
+      } else if constexpr (Q8) {
+        rv[c][0] = rv[c][1] = rv[c][2] = rv[c][3] = 0.f;
       }
     }
+    if constexpr (Q8) quant_row_fp8<RC_MAXC>(rv, amax, e5, q8 + r * ldq8, q8_scale + r, D, lane);
   }
 #pragma unroll
   for (int c = 0; c < RC_MAXC; ++c)
@@ -372,6 +388,27 @@ extern "C" int32_t maeclip_colsum_reduce(const float* partial, int64_t P, int64_
 
 
 extern "C" int32_t maeclip_rows_colsum_partial_rows(int64_t M) { return rows_colsum_grid(M); }
+
+extern "C" int32_t maeclip_rows_colsum_q8(const void* x, int32_t dtype, int64_t M, int64_t D, int64_t ld,
+                                          void* out_bf16, float* partial, void* q8, int64_t ldq8, float* q8_scale,
+                                          int32_t q8_fmt, void* stream) {
+  MC_CHECK_ARG(x && partial && out_bf16 && q8 && q8_scale && M >= 0 && D > 0 && D <= RC_MAXC * 256 && D % 4 == 0 &&
+                   ld >= D && ldq8 >= D && ldq8 % 4 == 0 && ((uintptr_t)q8 & 3) == 0 &&
+                   (dtype == MAECLIP_F32 || dtype == MAECLIP_BF16) &&
+                   (q8_fmt == MAECLIP_FP8_E4M3 || q8_fmt == MAECLIP_FP8_E5M2),
+               "maeclip_rows_colsum_q8: bad args");
+  if (M == 0) return 0;
+  dim3 grid((unsigned)rows_colsum_grid(M));
+  const bool e5 = q8_fmt == MAECLIP_FP8_E5M2;
+  if (dtype == MAECLIP_BF16)
+    hipLaunchKernelGGL((rows_colsum_kernel<bf16_t, true>), grid, dim3(NTH), 0, (hipStream_t)stream, (const bf16_t*)x, M,
+                       (int)D, ld, (bf16_t*)out_bf16, partial, (uint8_t*)q8, ldq8, q8_scale, e5);
+  else
+    hipLaunchKernelGGL((rows_colsum_kernel<float, true>), grid, dim3(NTH), 0, (hipStream_t)stream, (const float*)x, M,
+                       (int)D, ld, (bf16_t*)out_bf16, partial, (uint8_t*)q8, ldq8, q8_scale, e5);
+  MC_CHECK_LAUNCH("maeclip_rows_colsum_q8");
+  return 0;
+}
 
 // scratch floats maeclip_colsum_reduce needs for a [P, N] partial matrix
 extern "C" int64_t maeclip_colsum_scratch(int64_t P, int64_t N) {

@@ -57,25 +57,6 @@ template <typename YT> __device__ __forceinline__ float as_stored(float f) {
   return sizeof(YT) == 2 ? bf2f(f2bf(f)) : f;
 }
 
-// fp8 copy of a row held by one wave (lane: NC chunks of 4 at c * 256 + 4 lane),
-// bit-identical to maeclip_quant_rows_fp8 of the stored row: s = amax / MAX
-// (1 if amax = 0), q = rne(v / s)
-template <int NC>
-__device__ __forceinline__ void quant_row_fp8(const float (&v)[NC][4], float amax, bool e5, uint8_t* q, float* scale,
-                                              int D, int lane) {
-  amax = wave_max(amax);
-  const float s = amax > 0.f ? amax / (e5 ? MC_E5M2_MAX : MC_E4M3_MAX) : 1.f;
-  const float inv = 1.f / s;
-  if (lane == 0) *scale = s;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const int e = c * 256 + lane * 4;
-    if (e < D)
-      *(unsigned*)(q + e) = e5 ? mc_cvt4_fp8<true>(v[c][0] * inv, v[c][1] * inv, v[c][2] * inv, v[c][3] * inv)
-                               : mc_cvt4_fp8<false>(v[c][0] * inv, v[c][1] * inv, v[c][2] * inv, v[c][3] * inv);
-  }
-}
-
 __device__ __forceinline__ float keepf(uint64_t seed, int64_t row, int col, uint32_t thr, float sc) {
   return mc_hash4(seed, (uint64_t)row, (uint64_t)col, 0x4c4eull) >= thr ? sc : 0.f;
 }

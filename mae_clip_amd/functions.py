@@ -421,10 +421,12 @@ class TransformerStackFn(torch.autograd.Function):
         if not g.is_contiguous():
             g = g.contiguous()
         gT = torch.empty((M, D), device=g.device, dtype=torch.bfloat16) if bf else None
-        cpart = K.rows_colsum(g, out_bf16=gT)
+        # fp8 copy of gT for the top fc2 dgrad: made with gT here (fp8 mode), then
+        # by the LayerNorm backward that produces each next gT
+        gq = _q8(spec.w8[-1][3], M, D, _gfmt(), g.device) if (bf and spec.w8 is not None) else None
+        cpart = K.rows_colsum(g, out_bf16=gT, q8=gq)
         if not bf:
             gT = g
-        gq = None   # fp8 (e5m2) copy of gT made by the LayerNorm backward that produced it
         for i in reversed(range(len(spec.wT))):
             wqkv, wproj, w1, w2 = spec.wT[i]
             f8 = spec.w8[i] if spec.w8 is not None else (None,) * 4
@@ -507,7 +509,8 @@ class TransformerStackFn(torch.autograd.Function):
         if not g.is_contiguous():
             g = g.contiguous()
         gT = e((M, D))
-        cpart = K.rows_colsum(g, out_bf16=gT)
+        gq0 = _q8(spec.w8[-1][3], M, D, _gfmt(), dev) if spec.w8 is not None else None   # top fp8 operand
+        cpart = K.rows_colsum(g, out_bf16=gT, q8=gq0)
         # whole-batch gradient buffers of every block, written per micro-batch
         bufs = []
         for wqkv, wproj, w1, w2 in spec.wT:
@@ -520,7 +523,8 @@ class TransformerStackFn(torch.autograd.Function):
         mb.fork()
         # per micro-batch: (f32 residual gradient, its bf16 copy, the copy's fp8
         # rows from the LayerNorm backward that made it -- fp8 mode)
-        gin = [(g[slice(r0, r1)], gT[slice(r0, r1)], None) for r0, r1 in mb.rows]
+        gin = [(g[slice(r0, r1)], gT[slice(r0, r1)],
+                None if gq0 is None else K.Fp8Rows(gq0.q[r0:r1], gq0.s[r0:r1], gq0.fmt)) for r0, r1 in mb.rows]
         for i in reversed(range(len(spec.wT))):
             wqkv, wproj, w1, w2 = spec.wT[i]
             n1w, n2w = params[i * PER_BLOCK], params[i * PER_BLOCK + 6]

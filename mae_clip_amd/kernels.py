@@ -439,12 +439,17 @@ def colsum_reduce(partial, out=None, accumulate=False, scale=1.0):
     return out
 
 
-def rows_colsum(x, out_bf16=None):
-    """partial column sums [G, D] of x [M, D] (f32/bf16); optional bf16 copy."""
+def rows_colsum(x, out_bf16=None, q8=None):
+    """partial column sums [G, D] of x [M, D] (f32/bf16); optional bf16 copy
+    and (with it) its fp8 rows q8 (Fp8Rows, == quant_rows_fp8(out_bf16))."""
     _dev(x, out_bf16)
     M, D = x.shape
     G = int(L.lib().maeclip_rows_colsum_partial_rows(M))
     part = torch.empty((G, D), device=x.device, dtype=torch.float32)
+    if q8 is not None:
+        _call("maeclip_rows_colsum_q8", x.data_ptr(), _dt(x), M, D, x.stride(0), _ptr(out_bf16), part.data_ptr(),
+              q8.q.data_ptr(), q8.q.stride(0), q8.s.data_ptr(), q8.fmt, _stream())
+        return part
     _call("maeclip_rows_colsum", x.data_ptr(), _dt(x), M, D, x.stride(0), _ptr(out_bf16), part.data_ptr(), _stream())
     return part
 

@@ -65,6 +65,22 @@ def test_layernorm_fused_fp8_copy_bit_exact(dev, D, fmt):
     assert torch.equal(qb.s, rb.s) and torch.equal(qb.q, rb.q)
 
 
+@pytest.mark.parametrize("fmt", [K.FP8_E4M3, K.FP8_E5M2])
+def test_rows_colsum_fused_fp8_rows(dev, fmt):
+    """The fp8 stack's top gradient: rows_colsum writes the bf16 copy and its fp8
+    rows in one pass, bit-identical to quant_rows_fp8 of the bf16 copy."""
+    g = torch.Generator().manual_seed(5 + fmt)
+    x = (torch.randn(300, 1024, generator=g) * torch.logspace(-4, 2, 300).view(-1, 1)).to(dev)
+    x[9] = 0.0
+    xb = torch.empty_like(x, dtype=torch.bfloat16)
+    q = K.new_fp8_rows(300, 1024, fmt, dev)
+    part = K.rows_colsum(x, out_bf16=xb, q8=q)
+    r = K.quant_rows_fp8(xb, fmt)
+    assert torch.equal(q.q, r.q) and torch.equal(q.s, r.s)
+    assert torch.equal(xb, x.to(torch.bfloat16))
+    assert (part.sum(0) - x.sum(0)).abs().max().item() < 1e-3 * x.abs().max().item()
+
+
 def test_quant_cols_bit_exact(dev):
     g = torch.Generator().manual_seed(7)
     w = (torch.randn(200, 136, generator=g) * torch.logspace(-3, 1, 136)).to(dev)
