@@ -421,12 +421,24 @@ def u8_leg(model, opt, args, size, device, use_graph):
     runner.loss_value()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # the whole drop-in loop of main.py:54-66: the input copy of :55 AND the
+    # blocking loss read of :64 before the next step is queued
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step()
+        runner.loss_value()
+    torch.cuda.synchronize()
+    el_drop = time.perf_counter() - t0
     h2d = sum(v.numel() * v.element_size() for v in host.values())
     return {"value": round(B * steps / el, 2), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 3),
             "steps": steps, "h2d_bytes_per_step": h2d,
             "h2d_bytes_per_step_fp32_reference": B * 3 * size * size * 4 + 2 * B * T * 8,
             "what": "uint8 HWC pixels + text ids/mask copied host(pinned)->device inside every timed step "
-                    "(main.py:55), A.Normalize/permute fused into the patch gather and MAE target read"}
+                    "(main.py:55), A.Normalize/permute fused into the patch gather and MAE target read",
+            "drop_in_loop": {"value": round(B * steps / el_drop, 2), "unit": "images/s",
+                             "ms_per_step": round(el_drop / steps * 1e3, 3),
+                             "what": "the same copy inside every step plus each step's loss read (blocking) "
+                                     "before the next is queued: main.py:55 and :64 together"}}
 
 
 def spawn_ranks(n):
