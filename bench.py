@@ -467,8 +467,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
     ap.add_argument("--mask-ratio", type=float, default=None)
     ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
-                    help="GEMM operand precision (fp8: OCP e4m3 forward / e5m2 dgrad GEMMs of the encoder, "
-                         "per-row (activations) / per-channel (weights) current scaling)")
+                    help="GEMM operand precision (fp8: OCP e4m3 forward and dgrad GEMMs of the encoder "
+                         "(config.fp8_grad_format), e8m0 per-32 blocks / per-row scales on the activations, "
+                         "per-channel on the weights)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-kernel-timer", action="store_true")

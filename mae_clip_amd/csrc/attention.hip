@@ -112,6 +112,41 @@ __device__ __forceinline__ void load_imgs(char* const (&lds)[NI], const T* const
   }
 }
 
+// bf16 K / V images by LDS-DMA (buffer_load_dwordx4 ... lds): one
+// wave-instruction fills 1 KiB of an image, lane L the 16-B slot L of it, so
+// the XOR swizzle goes into the SOURCE address (slot s of row r holds chunk
+// s ^ f(r)); rows >= n read as zero through the descriptor's range check (its
+// extent ends with row n - 1's slice). No VGPR round trip and no per-chunk
+// address VALU beyond one row / chunk split per instruction; the wave waits for
+// its own DMA, the caller's barrier for everyone's. ATTN_NT: non-temporal
+// (aux bit 1) like the register path's loads.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+#ifndef ATTN_DMA
+#define ATTN_DMA 1
+#endif
+template <int HD>
+__device__ __forceinline__ void dma_imgs(char* Kimg, char* Vimg, const bf16_t* ks, const bf16_t* vs, int64_t ld,
+                                         int n, int npad) {
+  using I = Img<bf16_t, HD>;
+  const int64_t span = ((int64_t)(n - 1) * ld + HD) * 2;
+  const int nrec = (int)(span < 0x7fffffff ? span : 0x7fffffff);
+  const rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)ks, (short)0, nrec, 0x00020000);
+  const rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vs, (short)0, nrec, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nw = (int)(blockDim.x >> 6);
+  const int ninst = npad * I::CPR / 64;   // npad is a multiple of 64
+  for (int i = wave; i < ninst; i += nw) {
+    const int id = i * 64 + lane;
+    const int row = id / I::CPR, s = id % I::CPR;
+    const int voff = row * (int)ld * 2 + ((s ^ I::f(row)) << 4);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void_t*)(Kimg + i * 1024), 16, voff, 0, 0, ATTN_NT ? 2 : 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void_t*)(Vimg + i * 1024), 16, voff, 0, 0, ATTN_NT ? 2 : 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // dot product of two 16-B chunks in f32
 template <typename T> __device__ __forceinline__ float chunk_dot(v4u a, v4u b);
 template <> __device__ __forceinline__ float chunk_dot<bf16_t>(v4u a, v4u b) {
@@ -514,7 +549,9 @@ attn_fwd_kernel(const maeclip_attn_args a) {
 
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
   const int HH = H * HD;
-  {
+  if constexpr (std::is_same<T, bf16_t>::value && ATTN_DMA) {
+    dma_imgs<HD>(Kimg, Vimg, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
+  } else {
     char* const dst[2] = {Kimg, Vimg};
     const T* const src[2] = {qkv + HH + h * HD, qkv + 2 * HH + h * HD};
     load_imgs<T, HD, 2>(dst, src, a.ld_qkv, n, npad);
