@@ -150,10 +150,11 @@ class CLIPModel(nn.Module):
             dspec = Fn.DecSpec(B=B, L=L, keep=keep, dtype=dtype, w_T=cache.get(dec.decoder_embed.weight, dtype))
             xd = Fn.DecoderEmbedFn.apply(latent, ids_shuffle, ids_restore, dspec, dec.decoder_embed.weight,
                                          dec.decoder_embed.bias, dec.mask_token, dec.decoder_pos_embed)
-            # fp8 mode keeps the decoder on bf16: its K = 512 GEMMs are bound by
-            # their epilogue traffic, so fp8 operands would only add quantisation passes
+            # fp8 mode: the decoder stack on fp8 GEMMs too unless CFG.fp8_decoder is
+            # off (A/B in DESIGN.md Round 6: +1.9 %, its K = 512 GEMMs stay
+            # epilogue-bound)
             xd = run_stack(dec.decoder_layers, xd, dec.num_heads, dtype, cache,
-                           chunk=(CFG.dp_decoder_chunk or None) if world > 1 else None, fp8=False)
+                           chunk=(CFG.dp_decoder_chunk or None) if world > 1 else None, fp8=CFG.fp8_decoder)
             wp_T, bp_pad = cache.get(dec.decoder_pred.weight, dtype), None
             P = wp_T.shape[0]
             if dtype == torch.bfloat16 and P % 64:

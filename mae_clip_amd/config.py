@@ -69,6 +69,10 @@ fp8_grad_format = "e4m3"   # fp8 mode: the dgrad GEMMs' gradient operand, "e4m3"
 # fp8 mode: the attention (forward, backward) writes its output's fp8 blocks itself, else a standalone
 # quantisation pass (A/B in DESIGN.md; MAECLIP_FP8_ATTN_Q8="10" / "11" / "00" for the A/B runs)
 fp8_attn_q8 = tuple(c == "1" for c in __import__("os").environ.get("MAECLIP_FP8_ATTN_Q8", "11")[:2])
+# fp8 mode: the MAE decoder stack on fp8 GEMMs too (with the producers writing the fp8
+# operands, +1.9 % C4 fp8 and the same gradient error; MAECLIP_FP8_DECODER=0 for the
+# bf16 decoder; A/B in DESIGN.md Round 6)
+fp8_decoder = __import__("os").environ.get("MAECLIP_FP8_DECODER", "1") == "1"
 mask_seed = 2
 dropout_seed = 1234
 # ---- scheduling

@@ -596,4 +596,6 @@ class MAEDecoder(nn.Module):
         for blk in self.decoder_layers:
             for p in blk.gemm_weights():
                 cache.register(p, p.shape)
+                if CFG.fp8_decoder:
+                    cache.register_fp8(p)
         cache.register(self.decoder_pred.weight, self.decoder_pred.weight.shape)
