@@ -467,7 +467,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's)")
     ap.add_argument("--mask-ratio", type=float, default=None)
     ap.add_argument("--precision", choices=["bf16", "fp8"], default="bf16",
-                    help="GEMM operand precision (fp8: OCP e4m3 forward and dgrad GEMMs of the encoder "
+                    help="GEMM operand precision (fp8: OCP e4m3 forward and dgrad GEMMs of the encoder and decoder stacks "
                          "(config.fp8_grad_format), e8m0 per-32 blocks / per-row scales on the activations, "
                          "per-channel on the weights)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
