@@ -121,8 +121,8 @@ def test_product_data_parallel_equals_full_batch(dev, cfg):
 B_MB = 128   # samples per rank of the production-precision DP test (both stacks micro-batched)
 
 
-def _bf16_dp_rank(rank, world, port, out, grad_dtype):
-    """One gloo rank of the production-precision DP step: bf16 MFMA stacks run
+def _bf16_dp_rank(rank, world, port, out, grad_dtype, precision="bf16"):
+    """One gloo rank of the production-precision DP step: bf16 (or fp8) MFMA stacks run
     as two micro-batch chains each (B = 128 per rank: encoder 64 x 50, decoder
     64 x 197 rows per chain), the encoder / decoder cut into DP chunks
     (dp_*_chunk), gradients in the GradArena, all-reduced in fp32 or bf16
@@ -136,7 +136,7 @@ def _bf16_dp_rank(rank, world, port, out, grad_dtype):
         from mae_clip_amd.distributed import DataParallel
         from tests.helpers import make_batch
         _lib.load()
-        m = _model("bf16", cfg="C3")
+        m = _model(precision, cfg="C3")
         mb = [Fn.microbatch_count(Fn.StackSpec(B=B_MB, n=n, D=D, H=H, eps=1e-6, dtype=torch.bfloat16, wT=[]))
               for n, D, H in ((50, 768, 12), (197, 512, 16))]
         dp = DataParallel(m, bucket_mb=64.0, grad_dtype=torch.bfloat16 if grad_dtype == "bf16" else torch.float32)
@@ -153,8 +153,8 @@ def _bf16_dp_rank(rank, world, port, out, grad_dtype):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
-def test_product_data_parallel_bf16_microbatched(dev, grad_dtype):
+@pytest.mark.parametrize("precision,grad_dtype", [("bf16", "fp32"), ("bf16", "bf16"), ("fp8", "fp32")])
+def test_product_data_parallel_bf16_microbatched(dev, precision, grad_dtype):
     """The production DP step at world 2 (main.py:99-103's model and optimizer
     wrapped by distributed.DataParallel): C3 per-rank ViT-B/16 MAE+CLIP shapes
     in bf16 with micro-batched stacks and DP chunks, 2 gloo ranks on the one
@@ -162,17 +162,19 @@ def test_product_data_parallel_bf16_microbatched(dev, grad_dtype):
     (bf16, default settings). Loss within BF16_TOL["C2"][0] relative,
     gradients identical on both ranks, every gradient within BF16_TOL["C2"][1]
     relative L2 of the single process's; grad_dtype bf16 = the opt-in bf16
-    all-reduce buckets."""
+    all-reduce buckets; precision fp8 = the C4 mode's fp8 stacks (encoder and
+    decoder, per-row / per-block scales, which are row-local: a rank quantises
+    its rows as the single process does) on the same DP path."""
     from tests.helpers import make_batch, record_parity
     from tests.test_model_gpu import BF16_TOL
     loss_tol, grad_tol = BF16_TOL["C2"]
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_bf16_dp_rank, args=(2, _free_port(), out, grad_dtype), nprocs=2, join=True)
+    mp.spawn(_bf16_dp_rank, args=(2, _free_port(), out, grad_dtype, precision), nprocs=2, join=True)
     res = [out[r] for r in range(2)]
     assert all(r["microbatches"] == [2, 2] for r in res), [r["microbatches"] for r in res]
     assert res[0]["nbuckets"] >= 2
-    m = _model("bf16", cfg="C3")
+    m = _model(precision, cfg="C3")
     full = {k: v.to(dev) for k, v in make_batch(2 * B_MB, 224, seed=9).items()}
     loss = m(full)
     loss.backward()
@@ -192,7 +194,7 @@ def test_product_data_parallel_bf16_microbatched(dev, grad_dtype):
         e = ((res[0]["grads"][n] - g).norm() / (g.norm() + 1e-30)).item()
         if e > worst:
             worst, worst_name = e, n
-    record_parity(f"dp2_gloo_C3_bf16_microbatched_grad{grad_dtype}_vs_single_process", loss_rel=dl,
+    record_parity(f"dp2_gloo_C3_{precision}_microbatched_grad{grad_dtype}_vs_single_process", loss_rel=dl,
                   worst_grad_relL2=worst, worst_grad=worst_name)
     assert worst < grad_tol, (worst_name, worst)
 
