@@ -172,7 +172,9 @@ int32_t maeclip_quant_rows_fp8(const void* x, int32_t x_dtype, int64_t rows, int
 /* Every fp8 stack weight of a step at once (two launches): for each entry,
  * q = rows of W quantised per output channel (scales sq [rows]) and qt = W^T
  * quantised per input channel (scales sqt [cols], rows of ldqt bytes), from
- * the fp32 master W [rows, ld]. The host array is filled in by
+ * the fp32 master W [rows, ld], cols <= 4096 (the first launch keeps a row in
+ * registers: it quantises the rows and takes the column maxima from that one
+ * read; the second reads W again for W^T). The host array is filled in by
  * maeclip_quant_weights_fp8_prepare (prefix sums; returns the workspace
  * bytes); dev is its device copy. */
 typedef struct {

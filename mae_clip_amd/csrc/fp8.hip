@@ -193,92 +193,136 @@ __device__ __forceinline__ int wentry(const maeclip_fp8w_entry* __restrict__ e, 
   return lo;
 }
 
-// W rows (per output channel): one wave per row of the concatenated row space
-__device__ __forceinline__ void wq_rows(const maeclip_fp8w_entry* __restrict__ e, int n, int64_t total_rows,
-                                        int64_t blk) {
-  const int lane = threadIdx.x & 63;
-  const int64_t grow = blk * 4 + (threadIdx.x >> 6);
-  if (grow >= total_rows) return;
-  const maeclip_fp8w_entry& w = e[wentry(e, n, grow, false)];
-  const int64_t r = grow - w.row_begin;
-  const float* xr = w.w + r * w.ld;
-  const int cols = w.cols;
-  float amax = 0.f;
-  for (int c = lane * 8; c < cols; c += 512) {
-    float v[8];
-    Row8<float>::load(xr + c, v);
+// Launch 1: W rows (per output channel) AND the column partial maxima of W^T
+// from ONE read of W. A workgroup owns WQ_G consecutive rows of one entry (16
+// per wave, one row at a time in registers: cols <= 512 * RCH); every lane keeps
+// the running |max| of its 8 columns per 512-column chunk over the wave's rows,
+// the four waves' maxima meet in LDS, and the group writes one partial row
+// part[part_begin + g * cols + col] (g = the entry's group index). Entries'
+// row spaces are padded to WQ_G rows (row_begin), so no group straddles two.
+constexpr int WQ_G = 64;
+
+__global__ void __launch_bounds__(256) wq_rows_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
+                                                      float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t grow0 = (int64_t)blockIdx.x * WQ_G;
+  const maeclip_fp8w_entry& w = e[wentry(e, n, grow0, false)];
+  const int r0 = (int)(grow0 - w.row_begin);
+  const int cols = w.cols, nchunk = (cols + 511) / 512;
+  float cm[RCH][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[j]));
-  }
+  for (int c = 0; c < RCH; ++c)
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-  const float s = amax > 0.f ? amax / E4M3_MAX : 1.f;
-  const float inv = 1.f / s;
-  if (lane == 0) w.sq[r] = s;
-  uint8_t* qr = (uint8_t*)w.q + r * cols;
-  for (int c = lane * 8; c < cols; c += 512) {
-    float v[8];
-    Row8<float>::load(xr + c, v);
-    v2u o;
-    o[0] = cvt4<false>(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
-    o[1] = cvt4<false>(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv);
-    *(v2u*)(qr + c) = o;
+    for (int j = 0; j < 8; ++j) cm[c][j] = 0.f;
+  for (int i = 0; i < WQ_G / 4; ++i) {
+    const int r = r0 + wave * (WQ_G / 4) + i;
+    if (r >= w.rows) break;   // wave-uniform
+    const float* xr = w.w + (int64_t)r * w.ld;
+    float v[RCH][8];
+    float amax = 0.f;
+#pragma unroll
+    for (int c = 0; c < RCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (c < nchunk && col < cols) {
+        Row8<float>::load(xr + col, v[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = fabsf(v[c][j]);
+          amax = fmaxf(amax, a);
+          cm[c][j] = fmaxf(cm[c][j], a);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    const float s = amax > 0.f ? amax / E4M3_MAX : 1.f;
+    const float inv = 1.f / s;
+    if (lane == 0) w.sq[r] = s;
+    uint8_t* qr = (uint8_t*)w.q + (int64_t)r * cols;
+#pragma unroll
+    for (int c = 0; c < RCH; ++c) {
+      const int col = c * 512 + lane * 8;
+      if (c < nchunk && col < cols) {
+        v2u o;
+        o[0] = cvt4<false>(v[c][0] * inv, v[c][1] * inv, v[c][2] * inv, v[c][3] * inv);
+        o[1] = cvt4<false>(v[c][4] * inv, v[c][5] * inv, v[c][6] * inv, v[c][7] * inv);
+        *(v2u*)(qr + col) = o;
+      }
+    }
+  }
+  float* pr = part + w.part_begin + (int64_t)(r0 / WQ_G) * cols;
+#pragma unroll
+  for (int c = 0; c < RCH; ++c) {
+    if (c >= nchunk) break;   // block-uniform
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = cm[c][j];
+    __syncthreads();
+    for (int t = threadIdx.x; t < 512; t += 256) {
+      const int col = c * 512 + t;
+      if (col < cols) pr[col] = fmaxf(fmaxf(red[0][t], red[1][t]), fmaxf(red[2][t], red[3][t]));
+    }
+    __syncthreads();
   }
 }
 
-// W^T: units = (entry, 64-column strip, 256-row chunk), chunk fastest
-__device__ __forceinline__ void wq_cols_amax(const maeclip_fp8w_entry* __restrict__ e, int n,
-                                             float* __restrict__ part, int64_t gu, float (&red)[4][64]) {
-  const maeclip_fp8w_entry& w = e[wentry(e, n, gu, true)];
-  const int lu = (int)(gu - w.unit_begin), nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
-  const int c0 = (lu / nch) * 64, r0 = (lu % nch) * QC_ROWS;
-  const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6, col = c0 + tc;
-  float amax = 0.f;
-  if (col < w.cols)
-    for (int r = r0 + tr; r < min(w.rows, r0 + QC_ROWS); r += 4) amax = fmaxf(amax, fabsf(w.w[(int64_t)r * w.ld + col]));
-  red[tr][tc] = amax;
-  __syncthreads();
-  if (tr == 0 && col < w.cols)
-    part[w.part_begin + (int64_t)(lu % nch) * w.cols + col] =
-        fmaxf(fmaxf(red[0][tc], red[1][tc]), fmaxf(red[2][tc], red[3][tc]));
-}
-
-// one launch for both independent first passes: workgroups [0, rows_blocks)
-// quantise W rows, the rest take the partial column maxima of W^T
-__global__ void __launch_bounds__(256) wq_rows_amax_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
-                                                           int64_t total_rows, int64_t rows_blocks,
-                                                           float* __restrict__ part) {
-  __shared__ float red[4][64];
-  if ((int64_t)blockIdx.x < rows_blocks) wq_rows(e, n, total_rows, blockIdx.x);
-  else wq_cols_amax(e, n, part, (int64_t)blockIdx.x - rows_blocks, red);
-}
-
+// Launch 2: W^T. Units = (entry, 64-column strip, 256-row chunk), chunk
+// fastest; each reduces its strip's partials (fixed order) and writes its
+// 256 x 64 tile of W^T through LDS (the second and last read of W).
 __global__ void __launch_bounds__(256) wq_cols_kernel(const maeclip_fp8w_entry* __restrict__ e, int n,
                                                       const float* __restrict__ part) {
   __shared__ float tile[64][65];
   __shared__ float inv_s[64];
+  __shared__ float pmax[4][64];
   const int64_t gu = blockIdx.x;
   const maeclip_fp8w_entry& w = e[wentry(e, n, gu, true)];
   const int lu = (int)(gu - w.unit_begin), nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+  const int npart = (w.rows + WQ_G - 1) / WQ_G;
   const int c0 = (lu / nch) * 64, r0 = (lu % nch) * QC_ROWS;
   const int rows = w.rows, cols = w.cols;
-  if (threadIdx.x < 64) {
-    const int col = c0 + threadIdx.x;
-    float a = 0.f;
-    if (col < cols)
-      for (int k = 0; k < nch; ++k) a = fmaxf(a, part[w.part_begin + (int64_t)k * cols + col]);
-    const float s = a > 0.f ? a / E4M3_MAX : 1.f;
-    inv_s[threadIdx.x] = 1.f / s;
-    if (r0 == 0 && col < cols) w.sqt[col] = s;
-  }
   const int tc = threadIdx.x & 63, tr = threadIdx.x >> 6, col = c0 + tc;
-  uint8_t* qt = (uint8_t*)w.qt;
-  for (int rb = r0; rb < min(rows, r0 + QC_ROWS); rb += 64) {
-    __syncthreads();
-    for (int rr = tr; rr < 64; rr += 4) {
-      const int r = rb + rr;
-      tile[rr][tc] = (r < rows && col < cols) ? w.w[(int64_t)r * w.ld + col] : 0.f;
+  {
+    // the strip's column maxima: wave tr reduces partials tr, tr + 4, ...
+    // (4 loads in flight per lane), then the four meet in LDS (fixed order)
+    float a = 0.f;
+    if (col < cols) {
+      const float* pc = part + w.part_begin + col;
+      int k = tr;
+      for (; k + 12 < npart; k += 16)
+        a = fmaxf(fmaxf(a, fmaxf(pc[(int64_t)k * cols], pc[(int64_t)(k + 4) * cols])),
+                  fmaxf(pc[(int64_t)(k + 8) * cols], pc[(int64_t)(k + 12) * cols]));
+      for (; k < npart; k += 4) a = fmaxf(a, pc[(int64_t)k * cols]);
     }
+    pmax[tr][tc] = a;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const float m = fmaxf(fmaxf(pmax[0][tc], pmax[1][tc]), fmaxf(pmax[2][tc], pmax[3][tc]));
+      const float s = m > 0.f ? m / E4M3_MAX : 1.f;
+      inv_s[tc] = 1.f / s;
+      if (r0 == 0 && col < cols) w.sqt[col] = s;
+    }
+  }
+  uint8_t* qt = (uint8_t*)w.qt;
+  // 64 x 64 sub-tiles of W, 16-B loads (lane: 4 columns of rows t / 16 + 16 k),
+  // the next sub-tile's loads in flight while this one is transposed
+  const int lr = threadIdx.x >> 4, lc = (threadIdx.x & 15) * 4;
+  const int rend = min(rows, r0 + QC_ROWS);
+  auto ld4 = [&](int rb, v4f (&x)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = rb + lr + 16 * k;
+      x[k] = (r < rend && c0 + lc < cols) ? *(const v4f*)(w.w + (int64_t)r * w.ld + c0 + lc) : v4f{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  v4f nx[4];
+  ld4(r0, nx);
+  for (int rb = r0; rb < rend; rb += 64) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[lr + 16 * k][lc + j] = nx[k][j];
+    if (rb + 64 < rend) ld4(rb + 64, nx);
     __syncthreads();
     const int tc2 = threadIdx.x >> 2, seg = threadIdx.x & 3;
     const float inv = inv_s[tc2];
@@ -370,18 +414,19 @@ extern "C" int32_t maeclip_quant_blocks_fp8(const void* x, int32_t x_dtype, int6
   return 0;
 }
 
-// host side of the batched weight quantisation: prefix sums filled here
+// host side of the batched weight quantisation: prefix sums filled here (row
+// spaces padded to WQ_G rows; one partial row of column maxima per WQ_G rows)
 extern "C" int64_t maeclip_quant_weights_fp8_prepare(maeclip_fp8w_entry* host, int32_t n) {
   int64_t rows = 0, units = 0, part = 0;
   for (int i = 0; i < n; ++i) {
     maeclip_fp8w_entry& w = host[i];
-    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
+    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS, ng = (w.rows + WQ_G - 1) / WQ_G;
     w.row_begin = rows;
     w.unit_begin = units;
     w.part_begin = part;
-    rows += w.rows;
+    rows += (int64_t)ng * WQ_G;
     units += (int64_t)((w.cols + 63) / 64) * nch;
-    part += (int64_t)nch * w.cols;
+    part += (int64_t)ng * w.cols;
   }
   return part * 4;   // workspace bytes (column partial maxima)
 }
@@ -392,21 +437,20 @@ extern "C" int32_t maeclip_quant_weights_fp8(const maeclip_fp8w_entry* dev, cons
   int64_t rows = 0, units = 0, part = 0;
   for (int i = 0; i < n; ++i) {
     const maeclip_fp8w_entry& w = host[i];
-    MC_CHECK_ARG(w.w && w.q && w.sq && w.qt && w.sqt && w.rows > 0 && w.cols > 0 && w.cols % 8 == 0 &&
-                     w.ld >= w.cols && w.ld % 8 == 0 && w.ldqt >= w.rows && w.ldqt % 16 == 0,
-                 "maeclip_quant_weights_fp8: bad entry %d", i);
+    MC_CHECK_ARG(w.w && ((uintptr_t)w.w & 15) == 0 && w.q && w.sq && w.qt && w.sqt && w.rows > 0 && w.cols > 0 && w.cols % 8 == 0 &&
+                     w.cols <= 512 * RCH && w.ld >= w.cols && w.ld % 8 == 0 && w.ldqt >= w.rows && w.ldqt % 16 == 0,
+                 "maeclip_quant_weights_fp8: bad entry %d (16-B aligned w, cols %% 8, cols <= %d)", i, 512 * RCH);
     MC_CHECK_ARG(w.row_begin == rows && w.unit_begin == units && w.part_begin == part,
                  "maeclip_quant_weights_fp8: entries not prepared (maeclip_quant_weights_fp8_prepare)");
-    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS;
-    rows += w.rows;
+    const int nch = (w.rows + QC_ROWS - 1) / QC_ROWS, ng = (w.rows + WQ_G - 1) / WQ_G;
+    rows += (int64_t)ng * WQ_G;
     units += (int64_t)((w.cols + 63) / 64) * nch;
-    part += (int64_t)nch * w.cols;
+    part += (int64_t)ng * w.cols;
   }
   MC_CHECK_ARG(workspace && ws_bytes >= part * 4, "maeclip_quant_weights_fp8: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t rb = (rows + 3) / 4;
-  hipLaunchKernelGGL(wq_rows_amax_kernel, dim3((unsigned)(rb + units)), dim3(256), 0, s, dev, n, rows, rb, workspace);
-  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(rows + cols amax)");
+  hipLaunchKernelGGL(wq_rows_kernel, dim3((unsigned)(rows / WQ_G)), dim3(256), 0, s, dev, n, workspace);
+  MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(rows + column maxima)");
   hipLaunchKernelGGL(wq_cols_kernel, dim3((unsigned)units), dim3(256), 0, s, dev, n, (const float*)workspace);
   MC_CHECK_LAUNCH("maeclip_quant_weights_fp8(cols)");
   return 0;
