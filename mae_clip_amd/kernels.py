@@ -267,14 +267,17 @@ def quant_cols_fp8(w, out=None):
 
 class Fp8WeightPlan:
     """fp8 operands of a set of fp32 GEMM weights W [N, K], refreshed for all of
-    them in one maeclip_quant_weights_fp8 call (two launches): W per output
-    channel (forward B operand) and W^T per input channel (dgrad B operand)."""
+    them in one maeclip_quant_weights_fp8 call (two launches, W read twice): W
+    per output channel (forward B operand) and W^T per input channel (dgrad B
+    operand). Weights with K > 4096 (beyond the batched call's row registers)
+    take the per-weight quant_rows_fp8 / quant_cols_fp8 launches instead."""
+
+    WQ_MAX_COLS = 4096
 
     def __init__(self, weights, device):
-        n = len(weights)
         self.ops = []
-        self.host = (L.Fp8wEntry * n)()
-        for i, w in enumerate(weights):
+        batched, self.single = [], []
+        for w in weights:
             N, Kd = w.shape
             ldqt = (N + 15) // 16 * 16
             wq = Fp8Rows(torch.empty((N, Kd), device=device, dtype=torch.uint8),
@@ -282,18 +285,28 @@ class Fp8WeightPlan:
             wt = Fp8Rows(torch.empty((Kd, ldqt), device=device, dtype=torch.uint8)[:, :N],
                          torch.empty((Kd,), device=device, dtype=torch.float32), FP8_E4M3)
             self.ops.append((wq, wt))
-            e = self.host[i]
-            e.w, e.q, e.sq, e.qt, e.sqt = w.data_ptr(), wq.q.data_ptr(), wq.s.data_ptr(), wt.q.data_ptr(), wt.s.data_ptr()
-            e.rows, e.cols, e.ld, e.ldqt = N, Kd, w.stride(0), ldqt
-        nb = int(L.lib().maeclip_quant_weights_fp8_prepare(self.host, n))
-        self.ws_bytes = max(nb, 4)
-        self.ws = torch.empty((self.ws_bytes // 4,), device=device, dtype=torch.float32)
-        self.dev = torch.frombuffer(bytearray(bytes(self.host)), dtype=torch.uint8).to(device)
+            (batched if Kd <= self.WQ_MAX_COLS else self.single).append((w, wq, wt))
+        n = len(batched)
         self.n = n
+        if n:
+            self.host = (L.Fp8wEntry * n)()
+            for i, (w, wq, wt) in enumerate(batched):
+                e = self.host[i]
+                e.w, e.q, e.sq = w.data_ptr(), wq.q.data_ptr(), wq.s.data_ptr()
+                e.qt, e.sqt = wt.q.data_ptr(), wt.s.data_ptr()
+                e.rows, e.cols, e.ld, e.ldqt = w.shape[0], w.shape[1], w.stride(0), wt.q.stride(0)
+            nb = int(L.lib().maeclip_quant_weights_fp8_prepare(self.host, n))
+            self.ws_bytes = max(nb, 4)
+            self.ws = torch.empty((self.ws_bytes // 4,), device=device, dtype=torch.float32)
+            self.dev = torch.frombuffer(bytearray(bytes(self.host)), dtype=torch.uint8).to(device)
 
     def run(self):
-        _call("maeclip_quant_weights_fp8", self.dev.data_ptr(), self.host, self.n, self.ws.data_ptr(), self.ws_bytes,
-              _stream())
+        if self.n:
+            _call("maeclip_quant_weights_fp8", self.dev.data_ptr(), self.host, self.n, self.ws.data_ptr(),
+                  self.ws_bytes, _stream())
+        for w, wq, wt in self.single:
+            quant_rows_fp8(w, FP8_E4M3, out=wq)
+            quant_cols_fp8(w, out=wt)
 
 
 def gemm_fp8(A, B: Fp8Rows, Cout, epilogue=EPI_NONE, alpha=1.0, bias=None, aux=None, aux_out=None,

@@ -376,11 +376,13 @@ BF16_C4_TOL = 1.25e-2           # measured r03: 0.0061
 def test_batched_weight_quantisation_matches_single(dev):
     """maeclip_quant_weights_fp8 (all stack weights in two launches) ==
     the per-weight quant_rows_fp8 / quant_cols_fp8, bit for bit, over weights of
-    different shapes (row counts not multiples of 64 / 256)."""
+    different shapes (row counts not multiples of 64 / 256; K = 5120 is past the
+    batched call's 4096 columns and takes the per-weight launches)."""
     g = torch.Generator().manual_seed(3)
-    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096), (200, 136), (72, 512)]
+    shapes = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096), (200, 136), (72, 512), (96, 5120)]
     ws = [(torch.randn(s, generator=g) * torch.logspace(-2, 1, s[1])).to(dev) for s in shapes]
     plan = K.Fp8WeightPlan(ws, dev)
+    assert plan.n == len(shapes) - 1 and len(plan.single) == 1
     plan.run()
     for w, (wq, wt) in zip(ws, plan.ops):
         r = K.quant_rows_fp8(w, K.FP8_E4M3)
