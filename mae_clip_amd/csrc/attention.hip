@@ -125,24 +125,38 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef ATTN_DMA
 #define ATTN_DMA 1
 #endif
-template <int HD>
-__device__ __forceinline__ void dma_imgs(char* Kimg, char* Vimg, const bf16_t* ks, const bf16_t* vs, int64_t ld,
-                                         int n, int npad) {
+#ifndef ATTN_QIMG
+#define ATTN_QIMG 1
+#endif
+// forward: Q as a third LDS image (bf16 DMA path) only while two workgroups
+// per CU still fit with it: with one, the longer prologue has nothing to
+// overlap (C1 encoder n = 197 at hd 64: 95.6 -> 116.2 us; C4 decoder n = 577:
+// 233 -> 249 us), with two it saves a global round trip per query tile (C2
+// decoder 74.2 -> 67.6 us, C4 encoder 49.9 -> 47.3; profiles/r06/attn_fwd_qimg_ab_r6aa.txt)
+template <typename T, int HD> __host__ __device__ __forceinline__ bool fwd_qimg(int npad) {
+  return std::is_same<T, bf16_t>::value && ATTN_DMA && ATTN_QIMG &&
+         2 * (3 * npad * Img<T, HD>::ROWB + npad * 4) <= 163840;
+}
+
+template <int HD, int NI>
+__device__ __forceinline__ void dma_imgs(char* const (&dst)[NI], const bf16_t* const (&src)[NI], int64_t ld, int n,
+                                         int npad) {
   using I = Img<bf16_t, HD>;
   const int64_t span = ((int64_t)(n - 1) * ld + HD) * 2;
   const int nrec = (int)(span < 0x7fffffff ? span : 0x7fffffff);
-  const rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)ks, (short)0, nrec, 0x00020000);
-  const rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vs, (short)0, nrec, 0x00020000);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nw = (int)(blockDim.x >> 6);
   const int ninst = npad * I::CPR / 64;   // npad is a multiple of 64
-  for (int i = wave; i < ninst; i += nw) {
-    const int id = i * 64 + lane;
-    const int row = id / I::CPR, s = id % I::CPR;
-    const int voff = row * (int)ld * 2 + ((s ^ I::f(row)) << 4);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void_t*)(Kimg + i * 1024), 16, voff, 0, 0, ATTN_NT ? 2 : 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_void_t*)(Vimg + i * 1024), 16, voff, 0, 0, ATTN_NT ? 2 : 0);
+  for (int k = wave; k < ninst; k += nw) {
+    const int id = k * 64 + lane;
+    const int row = id / I::CPR, sl = id % I::CPR;
+    const int voff = row * (int)ld * 2 + ((sl ^ I::f(row)) << 4);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src[i], (short)0, nrec, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst[i] + k * 1024), 16, voff, 0, 0, ATTN_NT ? 2 : 0);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -531,10 +545,12 @@ __device__ __forceinline__ void q8_store(const maeclip_attn_args& a, int64_t row
 template <int A, int B> constexpr int cmax() { return A > B ? A : B; }
 // Q8: the fp8-blocks copy of o (maeclip_attn_args q8) from the kernel's own
 // stores -- its own instantiation, so the plain kernels keep their registers
-template <typename T, int HD, bool DROP, int WG = MAXW, bool Q8 = false>
+// QI: Q as a third LDS image (fwd_qimg; bf16, 8-wave launches only)
+template <typename T, int HD, bool DROP, int WG = MAXW, bool Q8 = false, bool QI = false>
 __global__ void __launch_bounds__(WG * 64)
 __attribute__((amdgpu_waves_per_eu(WG > MAXW ? cmax<fwd_wpe<T, HD, DROP>(), 4>() : fwd_wpe<T, HD, DROP>())))
 attn_fwd_kernel(const maeclip_attn_args a) {
+  static_assert(!QI || (std::is_same<T, bf16_t>::value && WG == MAXW), "QI: bf16, 8-wave launches");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using I = Img<T, HD>;
   const int n = a.n, H = a.H;
@@ -549,8 +565,20 @@ attn_fwd_kernel(const maeclip_attn_args a) {
 
   const T* qkv = (const T*)a.qkv + (int64_t)b * n * a.ld_qkv;
   const int HH = H * HD;
-  if constexpr (std::is_same<T, bf16_t>::value && ATTN_DMA) {
-    dma_imgs<HD>(Kimg, Vimg, qkv + HH + h * HD, qkv + 2 * HH + h * HD, a.ld_qkv, n, npad);
+  // bf16: the Q rows come as a third LDS image with K and V when two
+  // workgroups per CU still fit (fwd_qimg), so a query tile reads its Q
+  // fragments from LDS instead of a global round trip per tile
+  constexpr bool qimg = QI;
+  char* Qimg = smem + 2 * npad * I::ROWB + npad * 4;
+  if constexpr (qimg) {
+    char* const dst[3] = {Kimg, Vimg, Qimg};
+    const bf16_t* const src[3] = {(const bf16_t*)qkv + HH + h * HD, (const bf16_t*)qkv + 2 * HH + h * HD,
+                                  (const bf16_t*)qkv + h * HD};
+    dma_imgs<HD, 3>(dst, src, a.ld_qkv, n, npad);
+  } else if constexpr (std::is_same<T, bf16_t>::value && ATTN_DMA) {
+    char* const dst[2] = {Kimg, Vimg};
+    const bf16_t* const src[2] = {qkv + HH + h * HD, qkv + 2 * HH + h * HD};
+    dma_imgs<HD, 2>(dst, src, a.ld_qkv, n, npad);
   } else {
     char* const dst[2] = {Kimg, Vimg};
     const T* const src[2] = {qkv + HH + h * HD, qkv + 2 * HH + h * HD};
@@ -581,7 +609,10 @@ attn_fwd_kernel(const maeclip_attn_args a) {
     const bool qok = q < n;
     RowFrag<T, HD> qf[HD / 32];
 #pragma unroll
-    for (int ks = 0; ks < HD / 32; ++ks) qf[ks].glob(qkv + (int64_t)q * a.ld_qkv + h * HD, ks, lane, qok);
+    for (int ks = 0; ks < HD / 32; ++ks) {
+      if constexpr (qimg) qf[ks].lds(Qimg, qt * 16, ks, lane);
+      else qf[ks].glob(qkv + (int64_t)q * a.ld_qkv + h * HD, ks, lane, qok);
+    }
 
     float m = NEG_BIG, lsum = 0.f;
     v4f o[HD / 16], ol = {0.f, 0.f, 0.f, 0.f};
@@ -1451,7 +1482,8 @@ template <int HD> size_t bwd_diag_lds(int n) {
 
 template <typename T, int HD> size_t fwd_lds(int n) {
   const int npad = (n + 63) & ~63;
-  return (size_t)2 * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
+  const int nimg = fwd_qimg<T, HD>(npad) ? 3 : 2;   // K, V (+ Q; the 16-wave launches ignore the third)
+  return (size_t)nimg * npad * Img<T, HD>::ROWB + (size_t)npad * 4;
 }
 template <typename T, int HD> size_t bwd_lds(int n, int nw, bool two = false) {
   const int npad = (n + 31) & ~31;
@@ -1585,6 +1617,14 @@ int run(const maeclip_attn_args& a, bool bwd, hipStream_t s, bool& q8_done) {
     const bool q8 = std::is_same<T, bf16_t>::value && a.q8 != nullptr && a.dropout_p == 0.f;
     auto kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true>
                                   : (q8 ? attn_fwd_kernel<T, HD, false, MAXW, true> : attn_fwd_kernel<T, HD, false>);
+    if constexpr (std::is_same<T, bf16_t>::value) {
+      // (n <= 48: at most three query tiles, one per wave -- the DMA'd Q saves no
+      // round trip and lengthens the prologue: text n = 25 13.5 -> 15.5 us)
+      if (a.n > 48 && fwd_qimg<T, HD>((a.n + 63) & ~63))
+        kern = a.dropout_p > 0.f ? attn_fwd_kernel<T, HD, true, MAXW, false, true>
+                                 : (q8 ? attn_fwd_kernel<T, HD, false, MAXW, true, true>
+                                       : attn_fwd_kernel<T, HD, false, MAXW, false, true>);
+    }
     int nth = nthreads;
     // one workgroup per CU by LDS and more tiles than MAXW waves: up to 16
     // waves (option ATTN_FW16 = 0 turns it off)
